@@ -1,0 +1,195 @@
+/*
+ * rt.h — C ABI of the MI355X (gfx950) path-tracing hot path.
+ *
+ * Drop-in boundary for jalberse/RayTracingInOneWeekendInRust (crate `shimmer`):
+ * everything below `Renderer::render` (src/renderer.rs:42-105) — the per-pixel
+ * sample loop `Renderer::get_color` (src/renderer.rs:129-149), `Camera::get_ray`
+ * (src/camera.rs:96-106), `Ray::ray_color` (src/ray.rs:32-62), `Hittable::hit`
+ * for every geometry / acceleration type (src/hittable.rs, src/bvh.rs,
+ * src/aabb.rs, src/geometry/), `Material::scatter/emit` (src/materials/) and
+ * `Texture::value` (src/textures/) — runs as one HIP kernel launch per frame.
+ *
+ * The Rust side keeps its trait surface. Its scene (an `Arc<dyn Hittable>`
+ * graph) is lowered to the flat node IR below: one `rt_node` per reference
+ * constructor call (`Sphere::new`, `Bvh::new`, `RotateY::new`, ...), children
+ * referenced by node index. Shared `Arc`s are shared indices. INTEGRATION.md
+ * shows the `extern "C"` block the reference would add.
+ *
+ * Conventions
+ *  - Every entry point returns RT_OK (0) or a negative rt_status. On failure
+ *    rt_last_error() returns a per-thread message. No entry point aborts.
+ *  - Caller keeps ownership of every pointer it passes in; the library copies.
+ *  - Images are linear RGB f32, W*H*3, row 0 = the reference's y = 0 (the
+ *    bottom row; src/renderer.rs:141-142, written top-down by write_ppm).
+ */
+#ifndef RT_H
+#define RT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_ABI_VERSION 1
+
+typedef enum rt_status {
+    RT_OK = 0,
+    RT_ERR_INVALID = -1,     /* bad argument / malformed scene IR               */
+    RT_ERR_UNSUPPORTED = -2, /* IR shape the device path does not lower         */
+    RT_ERR_HIP = -3,         /* HIP runtime error (message has hipGetErrorString) */
+    RT_ERR_OOM = -4,         /* host or device allocation failed                */
+    RT_ERR_NO_DEVICE = -5,   /* no gfx950 device visible                        */
+    RT_ERR_IO = -6           /* asset file missing / unreadable                 */
+} rt_status;
+
+/* ------------------------------------------------------------------------ */
+/* Scene IR: one node per reference constructor call.                        */
+/* ------------------------------------------------------------------------ */
+typedef enum rt_node_kind {
+    /* textures — trait Texture, src/textures/texture.rs:3-5 */
+    RT_TEX_SOLID = 1,         /* f[0..3] color                      solid_color.rs:10   */
+    RT_TEX_CHECKER = 2,       /* f[0] scale, ref[0] even, ref[1] odd checker.rs:14      */
+    RT_TEX_MARBLE = 3,        /* f[0] scale, seed = Perlin seed      marble.rs:13        */
+    RT_TEX_IMAGE = 4,         /* ref[0] width, ref[1] height, seed = byte offset of the
+                                 RGB8 texels in rt_scene_desc.image_data  image_texture.rs:13 */
+    /* materials — trait Material, src/materials/material.rs:16-23 */
+    RT_MAT_LAMBERTIAN = 16,   /* ref[0] albedo texture               lambertian.rs:23    */
+    RT_MAT_METAL = 17,        /* f[0..3] albedo, f[3] fuzz (raw; clamped like metal.rs:20) */
+    RT_MAT_DIELECTRIC = 18,   /* f[0] index of refraction            dialectric.rs:19    */
+    RT_MAT_DIFFUSE_LIGHT = 19,/* ref[0] emission texture             diffuse_light.rs:14 */
+    RT_MAT_ISOTROPIC = 20,    /* ref[0] albedo texture               isotropic.rs:20     */
+    /* hittables — trait Hittable, src/hittable.rs:64-82 */
+    RT_OBJ_SPHERE = 32,       /* f[0..3] center, f[3] radius, ref[0] material  sphere.rs:26 */
+    RT_OBJ_MOVING_SPHERE = 33,/* f[0..3] c0, f[3..6] c1, f[6] t0, f[7] t1, f[8] radius,
+                                 ref[0] material                     moving_sphere.rs:29 */
+    RT_OBJ_XY_RECT = 34,      /* f = x0,x1,y0,y1,z ; ref[0] material rectangle.rs:24     */
+    RT_OBJ_XZ_RECT = 35,      /* f = x0,x1,z0,z1,y ; ref[0] material rectangle.rs:86     */
+    RT_OBJ_YZ_RECT = 36,      /* f = y0,y1,z0,z1,x ; ref[0] material rectangle.rs:148    */
+    RT_OBJ_CUBE = 37,         /* f[0..3] min, f[3..6] max, ref[0] material  cube.rs:23   */
+    RT_OBJ_TRI = 38,          /* f[0..9] p0,p1,p2, ref[0] material   triangle.rs:21      */
+    RT_OBJ_LIST = 39,         /* ref[0] first index into list_items, ref[1] count
+                                                                     hittable.rs:84-98   */
+    RT_OBJ_BVH = 40,          /* ref[0] LIST node, f[0] time0, f[1] time1,
+                                 seed = split-axis stream seed        bvh.rs:46-62        */
+    RT_OBJ_TRANSLATE = 41,    /* ref[0] child, f[0..3] displacement  instance.rs:23      */
+    RT_OBJ_ROTATE_Y = 42,     /* ref[0] child, f[0] degrees          instance.rs:63      */
+    RT_OBJ_CONSTANT_MEDIUM = 43 /* ref[0] boundary, ref[1] phase albedo texture,
+                                 f[0] density                        hittable.rs:150-174 */
+} rt_node_kind;
+
+typedef struct rt_node {
+    uint32_t kind;   /* rt_node_kind */
+    int32_t ref[3];  /* node indices (or counts, see kind); -1 = unused */
+    float f[12];     /* numeric constructor arguments */
+    uint64_t seed;   /* Perlin seed / BVH axis-stream seed / image byte offset */
+} rt_node;           /* 72 bytes, no padding */
+
+typedef struct rt_scene_desc {
+    const rt_node* nodes;
+    uint32_t num_nodes;
+    int32_t world;              /* index of the LIST node passed as `world` */
+    const int32_t* list_items;  /* children of LIST nodes, node indices */
+    uint32_t num_list_items;
+    uint32_t reserved0;
+    const uint8_t* image_data;  /* RGB8 texels of every RT_TEX_IMAGE */
+    uint64_t image_bytes;
+} rt_scene_desc;
+
+/* Raw arguments of Camera::new (src/camera.rs:44-81); the basis is derived
+ * on the host exactly as the reference does. */
+typedef struct rt_camera_desc {
+    float look_from[3];
+    float look_at[3];
+    float view_up[3];
+    float vfov_deg;
+    float aspect_ratio;
+    float aperture;
+    float focus_dist;
+    float time0;
+    float time1;
+} rt_camera_desc;
+
+#define RT_FLAG_EXACT_BVH 1u  /* box tests use the BVH entry t_max like bvh.rs:363-417
+                                 (no closest-hit pruning); results are identical
+                                 except for measure-zero ties, it is slower      */
+
+typedef struct rt_render_params {
+    uint32_t width, height;      /* image size (Renderer::from_aspect_ratio)        */
+    uint32_t samples_per_pixel;  /* spp, src/renderer.rs:140                        */
+    uint32_t max_depth;          /* ray_color depth, src/ray.rs:39-41               */
+    uint32_t tile_width, tile_height; /* Tile::tile decomposition (must be >= 1)    */
+    uint64_t seed;               /* Philox key of the per-sample random streams     */
+    uint32_t sample_base;        /* global index of this call's first sample        */
+    uint32_t shard_index;        /* this call renders the 8x8 pixel blocks b with   */
+    uint32_t shard_count;        /*   b % shard_count == shard_index (0/1 = all)    */
+    uint32_t flags;              /* RT_FLAG_*                                       */
+    float background[3];         /* src/main.rs:155-164                             */
+    uint32_t reserved1;
+} rt_render_params;
+
+typedef struct rt_stats {
+    uint64_t segments;    /* ray segments traced (world intersections)            */
+    uint64_t samples;     /* camera samples taken                                 */
+    double kernel_ms;     /* device time of the render launch (rt_render only)    */
+} rt_stats;
+
+typedef struct rt_tile {
+    uint32_t width, height, x_start, y_start;
+} rt_tile;
+
+typedef struct rt_scene* rt_scene_handle;
+
+/* ------------------------------------------------------------------------ */
+/* Entry points                                                              */
+/* ------------------------------------------------------------------------ */
+int rt_abi_version(void);
+const char* rt_last_error(void);
+int rt_device_count(int* count);
+
+/* Tile::tile, src/renderer.rs:242-296. Writes min(cap, n) tiles, returns n in *count. */
+int rt_tile_image(uint32_t image_width, uint32_t image_height, uint32_t tile_width,
+                  uint32_t tile_height, rt_tile* out, uint32_t cap, uint32_t* count);
+
+/* Lower the IR to device SoA buffers on `device` (one copy in HBM). */
+int rt_scene_upload(const rt_scene_desc* scene, int device, rt_scene_handle* out);
+int rt_scene_free(rt_scene_handle scene);
+/* counts: [entries, spheres, moving spheres, rects, tris, bvh nodes, materials,
+ *          textures, max bvh depth, device bytes] */
+int rt_scene_info(rt_scene_handle scene, uint64_t counts[10]);
+
+/* Asynchronous render on `stream` (hipStream_t, NULL = default stream) into a
+ * DEVICE buffer of W*H*3 floats; only the shard's pixels are written.
+ * d_segments (device uint64, may be NULL) is incremented by the segments traced. */
+int rt_render_launch(rt_scene_handle scene, const rt_camera_desc* camera,
+                     const rt_render_params* params, float* d_out,
+                     unsigned long long* d_segments, void* stream);
+
+/* Synchronous drop-in for Renderer::render minus the PPM write: renders into a
+ * HOST buffer of W*H*3 floats (pixels outside the shard are left untouched). */
+int rt_render(rt_scene_handle scene, const rt_camera_desc* camera,
+              const rt_render_params* params, float* host_out, rt_stats* stats);
+
+/* Scene builders restated from src/main.rs:185-829 ("random-spheres",
+ * "random-moving-spheres", "two-spheres", "marble", "earth", "simple-lights",
+ * "cornell", "cornell-smoke", "showcase", "bunny", "gargoyle", "igea-hrpp").
+ * asset_dir holds earthmap_1024x512.rgb8 and optional OBJ meshes.
+ * The returned descriptor owns its arrays; free with rt_scene_desc_free. */
+int rt_scene_generate(const char* name, uint64_t seed, const char* asset_dir,
+                      rt_scene_desc** out);
+void rt_scene_desc_free(rt_scene_desc* desc);
+/* Background of the CLI for `name` (src/main.rs:155-164). */
+int rt_scene_background(const char* name, float rgb[3]);
+
+/* Device numeric self-check (diagnostic): evaluates op on `n` inputs on the GPU.
+ * op: 0 sqrt f64, 1 sqrt f32, 2 div f32, 3 rt_sinf, 4 rt_acosf, 5 rt_atan2f,
+ *     6 rt_logf, 7 div f64. Results are returned as doubles. */
+int rt_device_numeric_eval(int op, const double* a, const double* b, double* out,
+                           uint32_t n);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RT_H */

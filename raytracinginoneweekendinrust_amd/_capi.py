@@ -1,0 +1,112 @@
+"""ctypes mirror of include/rt.h (the C ABI of the MI355X hot path).
+
+Loads the in-tree ``_lib/librtamd.so`` built by ``csrc/Makefile``. There is no
+Python or CPU fallback: if the library is missing, importing this module raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_DIR = os.path.join(_HERE, "_lib")
+LIB_PATH = os.path.join(LIB_DIR, "librtamd.so")
+ASSET_DIR = os.path.normpath(os.path.join(_HERE, "..", "assets"))
+
+# rt_node_kind
+RT_TEX_SOLID, RT_TEX_CHECKER, RT_TEX_MARBLE, RT_TEX_IMAGE = 1, 2, 3, 4
+RT_MAT_LAMBERTIAN, RT_MAT_METAL, RT_MAT_DIELECTRIC, RT_MAT_DIFFUSE_LIGHT, RT_MAT_ISOTROPIC = 16, 17, 18, 19, 20
+(RT_OBJ_SPHERE, RT_OBJ_MOVING_SPHERE, RT_OBJ_XY_RECT, RT_OBJ_XZ_RECT, RT_OBJ_YZ_RECT, RT_OBJ_CUBE, RT_OBJ_TRI,
+ RT_OBJ_LIST, RT_OBJ_BVH, RT_OBJ_TRANSLATE, RT_OBJ_ROTATE_Y, RT_OBJ_CONSTANT_MEDIUM) = range(32, 44)
+
+RT_FLAG_EXACT_BVH = 1
+
+STATUS = {0: "RT_OK", -1: "RT_ERR_INVALID", -2: "RT_ERR_UNSUPPORTED", -3: "RT_ERR_HIP", -4: "RT_ERR_OOM",
+          -5: "RT_ERR_NO_DEVICE", -6: "RT_ERR_IO"}
+
+
+class rt_node(C.Structure):
+    _fields_ = [("kind", C.c_uint32), ("ref", C.c_int32 * 3), ("f", C.c_float * 12), ("seed", C.c_uint64)]
+
+
+class rt_scene_desc(C.Structure):
+    _fields_ = [("nodes", C.POINTER(rt_node)), ("num_nodes", C.c_uint32), ("world", C.c_int32),
+                ("list_items", C.POINTER(C.c_int32)), ("num_list_items", C.c_uint32), ("reserved0", C.c_uint32),
+                ("image_data", C.POINTER(C.c_uint8)), ("image_bytes", C.c_uint64)]
+
+
+class rt_camera_desc(C.Structure):
+    _fields_ = [("look_from", C.c_float * 3), ("look_at", C.c_float * 3), ("view_up", C.c_float * 3),
+                ("vfov_deg", C.c_float), ("aspect_ratio", C.c_float), ("aperture", C.c_float),
+                ("focus_dist", C.c_float), ("time0", C.c_float), ("time1", C.c_float)]
+
+
+class rt_render_params(C.Structure):
+    _fields_ = [("width", C.c_uint32), ("height", C.c_uint32), ("samples_per_pixel", C.c_uint32),
+                ("max_depth", C.c_uint32), ("tile_width", C.c_uint32), ("tile_height", C.c_uint32),
+                ("seed", C.c_uint64), ("sample_base", C.c_uint32), ("shard_index", C.c_uint32),
+                ("shard_count", C.c_uint32), ("flags", C.c_uint32), ("background", C.c_float * 3),
+                ("reserved1", C.c_uint32)]
+
+
+class rt_stats(C.Structure):
+    _fields_ = [("segments", C.c_uint64), ("samples", C.c_uint64), ("kernel_ms", C.c_double)]
+
+
+class rt_tile(C.Structure):
+    _fields_ = [("width", C.c_uint32), ("height", C.c_uint32), ("x_start", C.c_uint32), ("y_start", C.c_uint32)]
+
+
+assert C.sizeof(rt_node) == 72
+assert C.sizeof(rt_render_params) == 64
+
+# (name, restype, argtypes) for every symbol declared in include/rt.h
+SIGNATURES = [
+    ("rt_abi_version", C.c_int, []),
+    ("rt_last_error", C.c_char_p, []),
+    ("rt_device_count", C.c_int, [C.POINTER(C.c_int)]),
+    ("rt_tile_image", C.c_int, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(rt_tile), C.c_uint32,
+                                C.POINTER(C.c_uint32)]),
+    ("rt_scene_upload", C.c_int, [C.POINTER(rt_scene_desc), C.c_int, C.POINTER(C.c_void_p)]),
+    ("rt_scene_free", C.c_int, [C.c_void_p]),
+    ("rt_scene_info", C.c_int, [C.c_void_p, C.POINTER(C.c_uint64)]),
+    ("rt_render_launch", C.c_int, [C.c_void_p, C.POINTER(rt_camera_desc), C.POINTER(rt_render_params), C.c_void_p,
+                                   C.c_void_p, C.c_void_p]),
+    ("rt_render", C.c_int, [C.c_void_p, C.POINTER(rt_camera_desc), C.POINTER(rt_render_params),
+                            C.POINTER(C.c_float), C.POINTER(rt_stats)]),
+    ("rt_scene_generate", C.c_int, [C.c_char_p, C.c_uint64, C.c_char_p, C.POINTER(C.POINTER(rt_scene_desc))]),
+    ("rt_scene_desc_free", None, [C.POINTER(rt_scene_desc)]),
+    ("rt_scene_background", C.c_int, [C.c_char_p, C.POINTER(C.c_float)]),
+    ("rt_device_numeric_eval", C.c_int, [C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double),
+                                         C.POINTER(C.c_double), C.c_uint32]),
+]
+
+
+def load() -> C.CDLL:
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(the MI355X path has no CPU fallback)")
+    lib = C.CDLL(LIB_PATH)
+    for name, res, args in SIGNATURES:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.rt_abi_version() != 1:
+        raise ImportError("librtamd.so ABI version mismatch")
+    return lib
+
+
+lib = load()
+
+
+class RTError(RuntimeError):
+    def __init__(self, code: int, where: str):
+        msg = lib.rt_last_error().decode(errors="replace")
+        super().__init__(f"{where}: {STATUS.get(code, code)}: {msg}")
+        self.code = code
+
+
+def check(code: int, where: str) -> None:
+    if code != 0:
+        raise RTError(code, where)

@@ -1,0 +1,128 @@
+// device_scene.hpp — layout of a lowered scene in HBM (host lowering <-> kernel).
+//
+// The reference walks an `Arc<dyn Hittable>` graph (src/hittable.rs:64-140).
+// Here the graph is flattened once on the host (lower.cpp) into:
+//   entries[]  the top-level HittableList in order (nested lists flattened,
+//              Translate/RotateY chains folded into each entry), followed by
+//              the boundaries of ConstantMedium entries;
+//   prims      SoA float4 records for spheres / moving spheres / rects / tris;
+//   nodes[]    every BVH (src/bvh.rs) as 32-byte nodes in DFS preorder;
+//   materials / textures / Perlin permutation tables / RGB8 texels.
+// Everything is read-only during a render and a few MB at most, so it stays
+// resident in each XCD's L2 after the first touch.
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIP__)
+#define RTDEV_HD __host__ __device__ inline
+#else
+#define RTDEV_HD inline
+#endif
+
+namespace rtdev {
+
+struct alignas(16) f4 {
+    float x, y, z, w;
+};
+
+// Child / leaf codes (BVH children, GEOM entry payloads, hit identifiers).
+// bit 31 set = leaf; bits 28..30 = leaf type; bits 0..27 = index.
+constexpr uint32_t kLeafBit = 0x80000000u;
+constexpr uint32_t kLeafSphere = 0u;   // index into sph
+constexpr uint32_t kLeafMSphere = 1u;  // index into msph (3 f4 each)
+constexpr uint32_t kLeafRect = 2u;     // index into rect (2 f4 each)
+constexpr uint32_t kLeafCube = 3u;     // index of the first of 6 rects (cube.rs:25-74 order)
+constexpr uint32_t kLeafTri = 4u;      // index into tri (3 f4 each)
+constexpr uint32_t kLeafMedium = 6u;   // hit identifier of a ConstantMedium scatter point
+constexpr uint32_t kChildEmpty = 0xffffffffu;  // second child of a 1-object node (bvh.rs:261-264)
+constexpr uint32_t kMaxIndex = 0x0fffffffu;
+
+RTDEV_HD uint32_t leaf_code(uint32_t type, uint32_t index) {
+    return kLeafBit | (type << 28) | index;
+}
+RTDEV_HD uint32_t leaf_type(uint32_t code) { return (code >> 28) & 7u; }
+RTDEV_HD uint32_t leaf_index(uint32_t code) { return code & kMaxIndex; }
+
+enum EntryKind : uint32_t {
+    kEntGeom = 0,    // payload = leaf code of one primitive / cube
+    kEntBvh = 1,     // payload = root node index
+    kEntMedium = 2,  // payload = boundary entry index; phase_mat, neg_inv_density
+};
+
+constexpr int kMaxTransforms = 3;
+
+// One top-level object (80 bytes). Transform ops are listed outer -> inner:
+//   w == 0: Translate by (x, y, z)   (instance.rs:32-43)
+//   w == 1: RotateY, x = sin, y = cos (instance.rs:114-143)
+struct alignas(16) DevEntry {
+    uint32_t kind;
+    uint32_t payload;
+    uint32_t ntf;
+    uint32_t phase_mat;
+    float neg_inv_density;
+    uint32_t pad[3];
+    f4 tf[kMaxTransforms];
+};
+static_assert(sizeof(DevEntry) == 80, "DevEntry layout");
+
+enum MatKind : uint32_t { kMatLambertian = 0, kMatMetal = 1, kMatDielectric = 2, kMatLight = 3, kMatIsotropic = 4 };
+struct alignas(16) DevMaterial {
+    uint32_t kind;
+    uint32_t tex;
+    float fuzz;
+    float ior;
+    float albedo[3];
+    float pad;
+};
+static_assert(sizeof(DevMaterial) == 32, "DevMaterial layout");
+
+enum TexKind : uint32_t { kTexSolid = 0, kTexChecker = 1, kTexMarble = 2, kTexImage = 3 };
+// checker: a = even, b = odd; marble: a = first of 9 permutation tables
+// (source, then distortion seeds 0..7); image: a = texel byte offset, b = w, c = h.
+struct alignas(16) DevTexture {
+    uint32_t kind;
+    uint32_t a, b, c;
+    float color[3];
+    float scale;
+};
+static_assert(sizeof(DevTexture) == 32, "DevTexture layout");
+
+// Record layouts (f4 units):
+//   sph  : (cx, cy, cz, r)                       + sph_mat[] (u32)
+//   msph : (c0, r) (c1 - c0, t0) (t1 - t0, mat, 0, 0)     moving_sphere.rs:47-51
+//   rect : (k, a0, a1, b0) (b1, axis, mat, 0)  axis 0 = XY, 1 = XZ, 2 = YZ
+//   tri  : (v0, mat) (v1 - v0, 0) (v2 - v0, 0)           triangle.rs:44-45
+//   node : (min, left) (max, right)   left/right: node index or leaf code
+struct DevScene {
+    const DevEntry* entries;
+    const f4* sph;
+    const uint32_t* sph_mat;
+    const f4* msph;
+    const f4* rect;
+    const f4* tri;
+    const f4* nodes;
+    const DevMaterial* mats;
+    const DevTexture* texs;
+    const uint8_t* perm;
+    const uint8_t* texels;
+    uint32_t num_top;
+    uint32_t num_entries;
+    uint32_t stack_depth;  // LDS traversal stack entries per lane
+    uint32_t pad;
+};
+
+// Camera::new (camera.rs:44-81) evaluated on the host.
+struct DevCamera {
+    float origin[3], horizontal[3], vertical[3], llc[3], u[3], v[3];
+    float lens_radius, time_low, time_scale;
+};
+
+struct DevParams {
+    uint32_t width, height, spp, max_depth;
+    uint32_t seed_lo, seed_hi, sample_base;
+    uint32_t shard_index, shard_count, blocks_x, num_blocks;
+    uint32_t flags;
+    float bg[3];
+};
+
+}  // namespace rtdev

@@ -1,0 +1,1094 @@
+// kernel.hip — the MI355X (gfx950 / CDNA4) path-tracing hot path.
+//
+// One 64-lane wave renders one 8x8 pixel block; lane = pixel. Each lane walks
+// its pixel's samples in order (src/renderer.rs:140-147) with PATH
+// REGENERATION: a lane whose path ends accumulates and immediately starts its
+// next camera sample, so every loop trip is one ray segment for every live
+// lane and no lane idles while a neighbour finishes a long path.
+//
+// Per segment (src/ray.rs:32-62): the top-level HittableList is walked in
+// order with a wave-uniform loop (entries are read with scalar loads), each
+// entry applies its Translate/RotateY chain, then tests a primitive, a cube, a
+// BVH (per-lane DFS stack in LDS, lane-strided so pushes never bank-conflict)
+// or a ConstantMedium. Only (t, entry, primitive) is kept per candidate; the
+// HitRecord of the winning candidate is rebuilt once, with the same arithmetic
+// the candidate test used, before Material::scatter / emit.
+//
+// Bit-exactness with the CPU oracle: built with -ffp-contract=off, correctly
+// rounded f32/f64 division and square root, rt_numeric_spec.h transcendentals,
+// and the reference's operation order (glam 0.22) everywhere. No MFMA: the path
+// has no dense contraction.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/rt.h"
+#include "../../include/rt_numeric_spec.h"
+#include "common.hpp"
+#include "device_scene.hpp"
+#include "lower.hpp"
+
+using rtdev::DevCamera;
+using rtdev::DevEntry;
+using rtdev::DevMaterial;
+using rtdev::DevParams;
+using rtdev::DevScene;
+using rtdev::DevTexture;
+using rtdev::f4;
+
+#define RT_DEV __device__ __forceinline__
+
+namespace {
+
+constexpr float kInf = __builtin_inff();
+
+// ---------------------------------------------------------------------------
+// vector math, glam 0.22 evaluation order
+// ---------------------------------------------------------------------------
+struct V {
+    float x, y, z;
+};
+RT_DEV V mk(float x, float y, float z) { return V{x, y, z}; }
+RT_DEV V operator+(V a, V b) { return V{a.x + b.x, a.y + b.y, a.z + b.z}; }
+RT_DEV V operator-(V a, V b) { return V{a.x - b.x, a.y - b.y, a.z - b.z}; }
+RT_DEV V operator*(V a, V b) { return V{a.x * b.x, a.y * b.y, a.z * b.z}; }
+RT_DEV V operator*(float s, V a) { return V{s * a.x, s * a.y, s * a.z}; }
+RT_DEV V operator-(V a) { return V{-a.x, -a.y, -a.z}; }
+RT_DEV V divs(V a, float s) { return V{a.x / s, a.y / s, a.z / s}; }
+RT_DEV float dot(V a, V b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
+RT_DEV V cross(V a, V b) { return V{a.y * b.z - b.y * a.z, a.z * b.x - b.z * a.x, a.x * b.y - b.x * a.y}; }
+RT_DEV float length(V a) { return __builtin_sqrtf(dot(a, a)); }
+RT_DEV V normalize(V a) {
+    float r = 1.0f / length(a);
+    return V{a.x * r, a.y * r, a.z * r};
+}
+RT_DEV float rs_min(float a, float b) {  // Rust f32::min (minnum)
+    if (a != a) return b;
+    if (b != b) return a;
+    return a < b ? a : b;
+}
+RT_DEV float rs_clamp(float x, float lo, float hi) {
+    if (x < lo) x = lo;
+    if (x > hi) x = hi;
+    return x;
+}
+RT_DEV bool sign_negative(float x) { return (__float_as_uint(x) >> 31) != 0u; }
+RT_DEV bool sign_negative_d(double x) { return (__double_as_longlong(x) >> 63) != 0; }
+RT_DEV V xyz(f4 a) { return V{a.x, a.y, a.z}; }
+RT_DEV f4 ld4(const f4* p) {
+    float4 v = *reinterpret_cast<const float4*>(p);
+    return f4{v.x, v.y, v.z, v.w};
+}
+
+struct Ray {
+    V o, d;
+    float time;
+};
+RT_DEV V at(const Ray& r, float t) { return r.o + t * r.d; }  // ray.rs:28-30
+
+// ---------------------------------------------------------------------------
+// Philox4x32-10 per-(pixel, sample) stream (replaces rand::thread_rng)
+// ---------------------------------------------------------------------------
+struct Rng {
+    uint32_t sample, pixel, block, n;
+    uint32_t b0, b1, b2, b3;
+};
+RT_DEV void philox(uint32_t& c0, uint32_t& c1, uint32_t& c2, uint32_t& c3, uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
+        uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
+        uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+}
+struct Key {
+    uint32_t k0, k1;
+};
+RT_DEV uint32_t next_u32(Rng& g, const Key& k) {
+    if (g.n == 0u) {
+        uint32_t c0 = g.block, c1 = g.sample, c2 = g.pixel, c3 = 0u;
+        philox(c0, c1, c2, c3, k.k0, k.k1);
+        g.b0 = c0; g.b1 = c1; g.b2 = c2; g.b3 = c3;
+        g.block += 1u;
+        g.n = 4u;
+    }
+    uint32_t r = g.b0;
+    g.b0 = g.b1; g.b1 = g.b2; g.b2 = g.b3;
+    g.n -= 1u;
+    return r;
+}
+RT_DEV float std01(Rng& g, const Key& k) {  // rand 0.8.5 Standard f32
+    return (1.0f / 16777216.0f) * (float)(next_u32(g, k) >> 8);
+}
+RT_DEV float from_1_2(uint32_t u) { return __uint_as_float((u >> 9) | 0x3f800000u); }
+RT_DEV float range_f(Rng& g, const Key& k, float low, float high) {  // UniformFloat::sample_single
+    float scale = high - low;
+    for (;;) {
+        float v01 = from_1_2(next_u32(g, k)) - 1.0f;
+        float res = v01 * scale + low;
+        if (res < high) return res;
+        scale = __uint_as_float(__float_as_uint(scale) - 1u);
+    }
+}
+RT_DEV V in_unit_sphere(Rng& g, const Key& k) {  // materials/utils.rs:6-19
+    for (;;) {
+        float x = range_f(g, k, -1.0f, 1.0f);
+        float y = range_f(g, k, -1.0f, 1.0f);
+        float z = range_f(g, k, -1.0f, 1.0f);
+        V v = mk(x, y, z);
+        if (dot(v, v) < 1.0f) return v;
+    }
+}
+RT_DEV V in_unit_disk(Rng& g, const Key& k) {  // utils.rs:9-17
+    for (;;) {
+        float x = range_f(g, k, -1.0f, 1.0f);
+        float y = range_f(g, k, -1.0f, 1.0f);
+        V p = mk(x, y, 0.0f);
+        if (dot(p, p) < 1.0f) return p;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// primitive tests: return the parameter t of the first valid root only
+// ---------------------------------------------------------------------------
+struct RayD {  // the f64 copy of a ray for sphere.rs:57-78, |d|^2 hoisted
+    double ox, oy, oz, dx, dy, dz, a;
+};
+RT_DEV RayD to_d(const Ray& r) {
+    RayD q;
+    q.ox = r.o.x; q.oy = r.o.y; q.oz = r.o.z;
+    q.dx = r.d.x; q.dy = r.d.y; q.dz = r.d.z;
+    q.a = (q.dx * q.dx + q.dy * q.dy) + q.dz * q.dz;
+    return q;
+}
+
+// sphere.rs:49-103 — quadratic in f64
+RT_DEV bool sphere_t(f4 s, const RayD& q, float tmin, float tmax, float& t) {
+    double ocx = q.ox - (double)s.x, ocy = q.oy - (double)s.y, ocz = q.oz - (double)s.z;
+    double rad = (double)s.w;
+    double half_b = (ocx * q.dx + ocy * q.dy) + ocz * q.dz;
+    double c = ((ocx * ocx + ocy * ocy) + ocz * ocz) - rad * rad;
+    double disc = half_b * half_b - q.a * c;
+    if (sign_negative_d(disc)) return false;
+    double sq = __builtin_sqrt(disc);
+    double root = (-half_b - sq) / q.a;
+    if (root < (double)tmin || (double)tmax < root) {
+        root = (-half_b + sq) / q.a;
+        if (root < (double)tmin || (double)tmax < root) return false;
+    }
+    t = (float)root;
+    return true;
+}
+
+// moving_sphere.rs:47-51
+RT_DEV V msphere_center(f4 m0, f4 m1, f4 m2, float time) {
+    float s = (time - m1.w) / m2.x;
+    return xyz(m0) + s * xyz(m1);
+}
+// moving_sphere.rs:54-84 — f32
+RT_DEV bool msphere_t(f4 m0, f4 m1, f4 m2, const Ray& r, float tmin, float tmax, float& t) {
+    V oc = r.o - msphere_center(m0, m1, m2, r.time);
+    float a = dot(r.d, r.d);
+    float half_b = dot(oc, r.d);
+    float c = dot(oc, oc) - m0.w * m0.w;
+    float disc = half_b * half_b - a * c;
+    if (sign_negative(disc)) return false;
+    float sq = __builtin_sqrtf(disc);
+    float root = (-half_b - sq) / a;
+    if (root < tmin || tmax < root) {
+        root = (-half_b + sq) / a;
+        if (root < tmin || tmax < root) return false;
+    }
+    t = root;
+    return true;
+}
+
+// rectangle.rs:36-65 / 98-127 / 160-189; axis 0 = XY (plane z), 1 = XZ (plane y), 2 = YZ (plane x)
+RT_DEV void rect_axes(uint32_t axis, const Ray& r, float& ok, float& dk, float& oa, float& da, float& ob,
+                      float& db) {
+    ok = axis == 0u ? r.o.z : (axis == 1u ? r.o.y : r.o.x);
+    dk = axis == 0u ? r.d.z : (axis == 1u ? r.d.y : r.d.x);
+    oa = axis == 2u ? r.o.y : r.o.x;
+    da = axis == 2u ? r.d.y : r.d.x;
+    ob = axis == 0u ? r.o.y : r.o.z;
+    db = axis == 0u ? r.d.y : r.d.z;
+}
+RT_DEV bool rect_t(f4 r0, f4 r1, const Ray& r, float tmin, float tmax, float& t) {
+    float ok, dk, oa, da, ob, db;
+    rect_axes(__float_as_uint(r1.y), r, ok, dk, oa, da, ob, db);
+    float tt = (r0.x - ok) / dk;
+    if (tt < tmin || tt > tmax) return false;
+    float x = oa + tt * da;
+    float y = ob + tt * db;
+    if (x < r0.y || x > r0.z || y < r0.w || y > r1.x) return false;
+    t = tt;
+    return true;
+}
+
+// triangle.rs:32-92 (Moller-Trumbore, eps 1e-7)
+RT_DEV bool tri_t(f4 t0, f4 t1, f4 t2, const Ray& r, float tmin, float tmax, float& t) {
+    const float eps = 0.0000001f;
+    V e1 = xyz(t1), e2 = xyz(t2);
+    V h = cross(r.d, e2);
+    float a = dot(e1, h);
+    if (a > -eps && a < eps) return false;
+    float f = 1.0f / a;
+    V s = r.o - xyz(t0);
+    float u = f * dot(s, h);
+    if (u < 0.0f || u > 1.0f) return false;
+    V q = cross(s, e1);
+    float v = f * dot(r.d, q);
+    if (v < 0.0f || u + v > 1.0f) return false;
+    float tt = f * dot(e2, q);
+    if (tt < tmin || tt > tmax) return false;
+    if (!(tt > eps)) return false;
+    t = tt;
+    return true;
+}
+
+// One leaf (primitive or cube). tmax = closest so far; a hit with t == closest is
+// accepted, so later candidates win ties exactly like hittable.rs:110-116.
+RT_DEV bool leaf_hit(const DevScene& S, uint32_t code, const Ray& r, const RayD& q, float tmin, float& closest,
+                     uint32_t& hit_code) {
+    uint32_t type = rtdev::leaf_type(code), idx = rtdev::leaf_index(code);
+    float t;
+    if (type == rtdev::kLeafSphere) {
+        if (sphere_t(ld4(S.sph + idx), q, tmin, closest, t)) {
+            closest = t;
+            hit_code = code;
+            return true;
+        }
+        return false;
+    }
+    if (type == rtdev::kLeafRect) {
+        if (rect_t(ld4(S.rect + 2 * idx), ld4(S.rect + 2 * idx + 1), r, tmin, closest, t)) {
+            closest = t;
+            hit_code = code;
+            return true;
+        }
+        return false;
+    }
+    if (type == rtdev::kLeafCube) {  // cube.rs:84-93: the six sides as a HittableList
+        bool any = false;
+        for (uint32_t i = 0; i < 6u; ++i) {
+            uint32_t ri = idx + i;
+            if (rect_t(ld4(S.rect + 2 * ri), ld4(S.rect + 2 * ri + 1), r, tmin, closest, t)) {
+                closest = t;
+                hit_code = rtdev::leaf_code(rtdev::kLeafRect, ri);
+                any = true;
+            }
+        }
+        return any;
+    }
+    if (type == rtdev::kLeafTri) {
+        if (tri_t(ld4(S.tri + 3 * idx), ld4(S.tri + 3 * idx + 1), ld4(S.tri + 3 * idx + 2), r, tmin, closest, t)) {
+            closest = t;
+            hit_code = code;
+            return true;
+        }
+        return false;
+    }
+    if (type == rtdev::kLeafMSphere) {
+        if (msphere_t(ld4(S.msph + 3 * idx), ld4(S.msph + 3 * idx + 1), ld4(S.msph + 3 * idx + 2), r, tmin, closest,
+                      t)) {
+            closest = t;
+            hit_code = code;
+            return true;
+        }
+    }
+    return false;
+}
+
+// aabb.rs:28-41 (Kensler). 1/d is hoisted per ray: the same IEEE quotient the
+// reference recomputes per node. All three slabs are evaluated branch-free; the
+// interval only shrinks, so this equals the reference's early-exit result.
+RT_DEV bool aabb_hit(f4 mn, f4 mx, const Ray& r, V inv, float t_min, float t_max) {
+    {
+        float t0 = (mn.x - r.o.x) * inv.x, t1 = (mx.x - r.o.x) * inv.x;
+        bool sw = inv.x < 0.0f;
+        float a = sw ? t1 : t0, b = sw ? t0 : t1;
+        t_min = a > t_min ? a : t_min;
+        t_max = b < t_max ? b : t_max;
+    }
+    {
+        float t0 = (mn.y - r.o.y) * inv.y, t1 = (mx.y - r.o.y) * inv.y;
+        bool sw = inv.y < 0.0f;
+        float a = sw ? t1 : t0, b = sw ? t0 : t1;
+        t_min = a > t_min ? a : t_min;
+        t_max = b < t_max ? b : t_max;
+    }
+    {
+        float t0 = (mn.z - r.o.z) * inv.z, t1 = (mx.z - r.o.z) * inv.z;
+        bool sw = inv.z < 0.0f;
+        float a = sw ? t1 : t0, b = sw ? t0 : t1;
+        t_min = a > t_min ? a : t_min;
+        t_max = b < t_max ? b : t_max;
+    }
+    return !(t_max < t_min);
+}
+
+// BvhNode::hit (bvh.rs:363-417) as an iterative left-first DFS. Visiting order
+// and tie rule are the reference's; box tests prune with the running closest
+// hit unless `exact` (then they use the t_max the BVH was entered with, as the
+// reference does). The stack lives in LDS: stack[level * 64 + lane].
+RT_DEV bool bvh_hit(const DevScene& S, uint32_t root, const Ray& r, float tmin, float& closest, uint32_t& hit_code,
+                    uint32_t* stk, bool exact) {
+    const float tmax_entry = closest;
+    V inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
+    RayD q = to_d(r);
+    bool any = false;
+    uint32_t sp = 0;
+    uint32_t cur = root;
+    for (;;) {
+        if (!(cur & rtdev::kLeafBit)) {
+            f4 a = ld4(S.nodes + 2 * cur), b = ld4(S.nodes + 2 * cur + 1);
+            if (aabb_hit(a, b, r, inv, tmin, exact ? tmax_entry : closest)) {
+                uint32_t right = __float_as_uint(b.w);
+                if (right != rtdev::kChildEmpty) {
+                    stk[sp * 64u] = right;
+                    sp += 1u;
+                }
+                cur = __float_as_uint(a.w);
+                continue;
+            }
+        } else {
+            any |= leaf_hit(S, cur, r, q, tmin, closest, hit_code);
+        }
+        if (sp == 0u) break;
+        sp -= 1u;
+        cur = stk[sp * 64u];
+    }
+    return any;
+}
+
+// Translate (instance.rs:39) / RotateY (instance.rs:104-110, 121-124) applied to a ray.
+RT_DEV Ray apply_op(f4 op, Ray r) {
+    if (op.w == 0.0f) {
+        r.o = r.o - xyz(op);
+    } else {
+        float s = op.x, c = op.y;
+        r.o = mk(c * r.o.x - s * r.o.z, r.o.y, s * r.o.x + c * r.o.z);
+        r.d = mk(c * r.d.x - s * r.d.z, r.d.y, s * r.d.x + c * r.d.z);
+    }
+    return r;
+}
+
+// A GEOM or BVH entry (the caller guarantees E is wave-uniform).
+RT_DEV bool entry_geom_hit(const DevScene& S, const DevEntry* E, Ray r, float tmin, float& closest,
+                           uint32_t& hit_code, uint32_t* stk, bool exact) {
+    uint32_t ntf = E->ntf;
+    for (uint32_t i = 0; i < ntf; ++i) r = apply_op(E->tf[i], r);
+    if (E->kind == rtdev::kEntBvh) return bvh_hit(S, E->payload, r, tmin, closest, hit_code, stk, exact);
+    RayD q = to_d(r);
+    return leaf_hit(S, E->payload, r, q, tmin, closest, hit_code);
+}
+
+// ConstantMedium::hit (hittable.rs:176-233); draws one U(0,1) once the clamped
+// interval is non-empty, exactly where the reference does.
+RT_DEV bool medium_hit(const DevScene& S, const DevEntry* E, Ray r, float tmin, float tmax, Rng& g, const Key& k,
+                       float& t_out, uint32_t* stk, bool exact) {
+    uint32_t ntf = E->ntf;
+    for (uint32_t i = 0; i < ntf; ++i) r = apply_op(E->tf[i], r);
+    const DevEntry* B = S.entries + E->payload;
+    float t1 = kInf, t2 = kInf;
+    uint32_t dummy;
+    if (!entry_geom_hit(S, B, r, -kInf, t1, dummy, stk, exact)) return false;
+    if (!entry_geom_hit(S, B, r, t1 + 0.0001f, t2, dummy, stk, exact)) return false;
+    if (t1 < tmin) t1 = tmin;
+    if (t2 > tmax) t2 = tmax;
+    if (t1 >= t2) return false;
+    if (t1 < 0.0f) t1 = 0.0f;
+    float ray_length = length(r.d);
+    float distance_inside = (t2 - t1) * ray_length;
+    float hit_distance = E->neg_inv_density * rt_logf(std01(g, k));
+    if (hit_distance > distance_inside) return false;
+    t_out = t1 + hit_distance / ray_length;
+    return true;
+}
+
+// HittableList::hit over the world (hittable.rs:100-118), t in [0.001, inf).
+RT_DEV bool world_hit(const DevScene& S, const Ray& r, Rng& g, const Key& k, float& t_hit, uint32_t& hit_entry,
+                      uint32_t& hit_code, uint32_t* stk, bool exact) {
+    float closest = kInf;
+    bool any = false;
+    for (uint32_t e = 0; e < S.num_top; ++e) {
+        const DevEntry* E = S.entries + e;
+        if (E->kind == rtdev::kEntMedium) {
+            float t;
+            if (medium_hit(S, E, r, 0.001f, closest, g, k, t, stk, exact)) {
+                closest = t;
+                hit_entry = e;
+                hit_code = rtdev::leaf_code(rtdev::kLeafMedium, 0);
+                any = true;
+            }
+        } else {
+            uint32_t code;
+            if (entry_geom_hit(S, E, r, 0.001f, closest, code, stk, exact)) {
+                hit_entry = e;
+                hit_code = code;
+                any = true;
+            }
+        }
+    }
+    t_hit = closest;
+    return any;
+}
+
+// ---------------------------------------------------------------------------
+// HitRecord reconstruction (hittable.rs:28-52 + each primitive's tail)
+// ---------------------------------------------------------------------------
+struct Rec {
+    V p, n;
+    float t, u, v;
+    bool front;
+    uint32_t mat;
+};
+RT_DEV void sphere_uv(V p, float& u, float& v) {  // sphere.rs:41-46
+    const float PI = 3.14159265358979323846f;
+    const float TWO_PI = 2.0f * PI;
+    float theta = rt_acosf(-p.y);
+    float phi = rt_atan2f(-p.z, p.x) + PI;
+    u = phi / TWO_PI;
+    v = theta / PI;
+}
+RT_DEV void rec_new(Rec& rec, const Ray& r, V outward, float t, float u, float v, uint32_t mat) {
+    rec.p = at(r, t);
+    rec.front = sign_negative(dot(r.d, outward));
+    rec.n = rec.front ? outward : -outward;
+    rec.t = t;
+    rec.u = u;
+    rec.v = v;
+    rec.mat = mat;
+}
+RT_DEV void prim_record(const DevScene& S, uint32_t code, const Ray& r, float t, Rec& rec) {
+    uint32_t type = rtdev::leaf_type(code), idx = rtdev::leaf_index(code);
+    if (type == rtdev::kLeafSphere) {
+        f4 s = ld4(S.sph + idx);
+        V p = at(r, t);
+        V n = divs(p - xyz(s), s.w);
+        float u, v;
+        sphere_uv(n, u, v);
+        rec_new(rec, r, n, t, u, v, S.sph_mat[idx]);
+    } else if (type == rtdev::kLeafRect) {
+        f4 r0 = ld4(S.rect + 2 * idx), r1 = ld4(S.rect + 2 * idx + 1);
+        uint32_t axis = __float_as_uint(r1.y);
+        float ok, dk, oa, da, ob, db;
+        rect_axes(axis, r, ok, dk, oa, da, ob, db);
+        float x = oa + t * da, y = ob + t * db;
+        float u = (x - r0.y) / (r0.z - r0.y);
+        float v = (y - r0.w) / (r1.x - r0.w);
+        V n = axis == 0u ? mk(0.0f, 0.0f, 1.0f) : (axis == 1u ? mk(0.0f, 1.0f, 0.0f) : mk(1.0f, 0.0f, 0.0f));
+        rec_new(rec, r, n, t, u, v, __float_as_uint(r1.z));
+    } else if (type == rtdev::kLeafTri) {
+        f4 t0 = ld4(S.tri + 3 * idx), t1 = ld4(S.tri + 3 * idx + 1), t2 = ld4(S.tri + 3 * idx + 2);
+        V n = normalize(cross(xyz(t1), xyz(t2)));
+        rec_new(rec, r, n, t, 0.0f, 0.0f, __float_as_uint(t0.w));
+    } else {  // moving sphere
+        f4 m0 = ld4(S.msph + 3 * idx), m1 = ld4(S.msph + 3 * idx + 1), m2 = ld4(S.msph + 3 * idx + 2);
+        V p = at(r, t);
+        V n = divs(p - msphere_center(m0, m1, m2, r.time), m0.w);
+        float u, v;
+        sphere_uv(n, u, v);
+        rec_new(rec, r, n, t, u, v, __float_as_uint(m2.y));
+    }
+}
+RT_DEV void make_record(const DevScene& S, uint32_t entry, uint32_t code, float t, const Ray& r0, Rec& rec) {
+    const DevEntry* E = S.entries + entry;
+    uint32_t ntf = E->ntf;
+    f4 op0 = E->tf[0], op1 = E->tf[1], op2 = E->tf[2];
+    Ray r1 = ntf > 0u ? apply_op(op0, r0) : r0;
+    Ray r2 = ntf > 1u ? apply_op(op1, r1) : r1;
+    Ray r3 = ntf > 2u ? apply_op(op2, r2) : r2;
+    if (rtdev::leaf_type(code) == rtdev::kLeafMedium) {  // hittable.rs:216-230
+        rec.t = t;
+        rec.p = at(r3, t);
+        rec.n = mk(1.0f, 0.0f, 0.0f);
+        rec.u = 0.0f;
+        rec.v = 0.0f;
+        rec.front = true;
+        rec.mat = E->phase_mat;
+    } else {
+        prim_record(S, code, r3, t, rec);
+    }
+    // unwind the chain inner -> outer (instance.rs:41, 128-140)
+#pragma unroll
+    for (int i = 2; i >= 0; --i) {
+        if ((uint32_t)i >= ntf) continue;
+        f4 op = i == 0 ? op0 : (i == 1 ? op1 : op2);
+        V dlev = i == 0 ? r1.d : (i == 1 ? r2.d : r3.d);  // the ray RotateY passed down
+        if (op.w == 0.0f) {
+            rec.p = rec.p + xyz(op);
+        } else {
+            float s = op.x, c = op.y;
+            V p = mk(c * rec.p.x + s * rec.p.z, rec.p.y, -s * rec.p.x + c * rec.p.z);
+            V n = mk(c * rec.n.x + s * rec.n.z, rec.n.y, -s * rec.n.x + c * rec.n.z);
+            rec.p = p;
+            bool ff = dot(dlev, n) < 0.0f;  // set_face_normal(&ray_rotated, normal)
+            rec.n = ff ? n : -n;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// textures (src/textures/*) — Marble restates noise 0.8.2 Perlin/Turbulence
+// ---------------------------------------------------------------------------
+RT_DEV uint32_t perm_hash(const uint8_t* t, int64_t x, int64_t y, int64_t z) {
+    uint32_t a = t[(uint32_t)(x & 0xff)];
+    a = t[a ^ (uint32_t)(y & 0xff)];
+    return t[a ^ (uint32_t)(z & 0xff)];
+}
+RT_DEV double surflet(uint32_t h, double dx, double dy, double dz) {
+    const double D = 0.7071067811865476;
+    double t = 1.0 - ((dx * dx + dy * dy) + dz * dz) * 2.0;
+    if (!(t > 0.0)) return 0.0;
+    uint32_t g = h % 12u;
+    // grad3: (+-D, +-D, 0) for 0..3, (+-D, 0, +-D) for 4..7, (0, +-D, +-D) for 8..11
+    double gx = g < 8u ? ((g & 2u) ? -D : D) : 0.0;
+    double gy = g < 4u ? ((g & 1u) ? -D : D) : (g < 8u ? 0.0 : ((g & 2u) ? -D : D));
+    double gz = g < 4u ? 0.0 : ((g & 1u) ? -D : D);
+    double t2 = t * t;
+    double t4 = t2 * t2;
+    return (2.0 * t2 + t4) * ((dx * gx + dy * gy) + dz * gz);
+}
+RT_DEV double perlin3(const uint8_t* t, double px, double py, double pz) {
+    const double SCALE = 1.1547005383792515;
+    double fx = __builtin_floor(px), fy = __builtin_floor(py), fz = __builtin_floor(pz);
+    int64_t ix = (int64_t)fx, iy = (int64_t)fy, iz = (int64_t)fz;
+    double dx = px - fx, dy = py - fy, dz = pz - fz;
+    double ex = dx - 1.0, ey = dy - 1.0, ez = dz - 1.0;
+    double r = surflet(perm_hash(t, ix, iy, iz), dx, dy, dz);
+    r = r + surflet(perm_hash(t, ix + 1, iy, iz), ex, dy, dz);
+    r = r + surflet(perm_hash(t, ix, iy + 1, iz), dx, ey, dz);
+    r = r + surflet(perm_hash(t, ix + 1, iy + 1, iz), ex, ey, dz);
+    r = r + surflet(perm_hash(t, ix, iy, iz + 1), dx, dy, ez);
+    r = r + surflet(perm_hash(t, ix + 1, iy, iz + 1), ex, dy, ez);
+    r = r + surflet(perm_hash(t, ix, iy + 1, iz + 1), dx, ey, ez);
+    r = r + surflet(perm_hash(t, ix + 1, iy + 1, iz + 1), ex, ey, ez);
+    r = r * SCALE;
+    if (r < -1.0) r = -1.0;
+    if (r > 1.0) r = 1.0;
+    return r;
+}
+RT_DEV double fbm_get(const uint8_t* tabs, uint32_t seed0, double x, double y, double z) {
+    const double lacunarity = 3.141592653589793 * 2.0 / 3.0;
+    double denom = 0.0, pw = 1.0;
+    for (int i = 1; i <= 6; ++i) {
+        pw = pw * 0.5;
+        denom = denom + pw;
+    }
+    const double scale_factor = 1.0 / denom;
+    double result = 0.0, persist = 1.0;
+    x = x * 1.0; y = y * 1.0; z = z * 1.0;
+    for (uint32_t o = 0; o < 6u; ++o) {
+        double signal = perlin3(tabs + 256u * (1u + seed0 + o), x, y, z);
+        signal = signal * persist;
+        result = result + signal;
+        persist = persist * 0.5;
+        x = x * lacunarity; y = y * lacunarity; z = z * lacunarity;
+    }
+    return result * scale_factor;
+}
+RT_DEV double turbulence(const uint8_t* tabs, double px, double py, double pz) {
+    const double power = 1.0;
+    double xd = px + fbm_get(tabs, 0u, px + 12414.0 / 65536.0, py + 65124.0 / 65536.0, pz + 31337.0 / 65536.0) * power;
+    double yd = py + fbm_get(tabs, 1u, px + 26519.0 / 65536.0, py + 18128.0 / 65536.0, pz + 60493.0 / 65536.0) * power;
+    double zd = pz + fbm_get(tabs, 2u, px + 53820.0 / 65536.0, py + 11213.0 / 65536.0, pz + 44845.0 / 65536.0) * power;
+    return perlin3(tabs, xd, yd, zd);
+}
+RT_DEV V tex_value(const DevScene& S, uint32_t tid, float u, float v, V p) {
+    for (;;) {
+        const DevTexture* T = S.texs + tid;
+        uint32_t kind = T->kind;
+        if (kind == rtdev::kTexSolid) return mk(T->color[0], T->color[1], T->color[2]);  // solid_color.rs:21-25
+        if (kind == rtdev::kTexChecker) {                                                  // checker.rs:27-37
+            float sc = T->scale;
+            float sines = rt_sinf(sc * p.x) * rt_sinf(sc * p.y) * rt_sinf(sc * p.z);
+            tid = sign_negative(sines) ? T->b : T->a;
+            continue;
+        }
+        if (kind == rtdev::kTexMarble) {  // marble.rs:23-29
+            double n = turbulence(S.perm + 256u * T->a, (double)p.x, (double)p.y, (double)p.z);
+            float s = 0.5f * (1.0f + rt_sinf(T->scale * p.z + 10.0f * (float)n));
+            return mk(s, s, s);
+        }
+        // image_texture.rs:21-52
+        uint32_t w = T->b, h = T->c;
+        float uu = rs_clamp(u, 0.0f, 1.0f);
+        float vv = 1.0f - rs_clamp(v, 0.0f, 1.0f);
+        uint32_t i = rt_f32_to_u32_sat(uu * (float)w);
+        uint32_t j = rt_f32_to_u32_sat(vv * (float)h);
+        if (i >= w) i = w - 1u;
+        if (j >= h) j = h - 1u;
+        const uint8_t* px = S.texels + T->a + ((size_t)j * w + i) * 3u;
+        const float cs = 1.0f / 255.0f;
+        return mk((float)px[0] * cs, (float)px[1] * cs, (float)px[2] * cs);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// materials (src/materials/*)
+// ---------------------------------------------------------------------------
+RT_DEV V reflect(V v, V n) { return v - (2.0f * dot(v, n)) * n; }  // utils.rs:37-39
+RT_DEV V refract(V uv, V n, float eta) {                          // utils.rs:41-46
+    float cos_t = rs_min(dot(-uv, n), 1.0f);
+    V r_perp = eta * (uv + cos_t * n);
+    V r_par = (-__builtin_sqrtf(__builtin_fabsf(1.0f - dot(r_perp, r_perp)))) * n;
+    return r_par + r_perp;
+}
+RT_DEV bool near_zero(V v) {  // utils.rs:5-7
+    const float eps = 1.1920929e-07f;
+    return __builtin_fabsf(v.x) < eps && __builtin_fabsf(v.y) < eps && __builtin_fabsf(v.z) < eps;
+}
+RT_DEV bool scatter(const DevScene& S, const DevMaterial& m, const Ray& r, const Rec& rec, Rng& g, const Key& k,
+                    V& att, Ray& sc) {
+    sc.o = rec.p;
+    sc.time = r.time;
+    if (m.kind == rtdev::kMatLambertian) {  // lambertian.rs:34-53
+        V dir = rec.n + normalize(in_unit_sphere(g, k));
+        if (near_zero(dir)) dir = rec.n;
+        sc.d = dir;
+        att = tex_value(S, m.tex, rec.u, rec.v, rec.p);
+        return true;
+    }
+    if (m.kind == rtdev::kMatMetal) {  // metal.rs:25-43
+        V reflected = reflect(normalize(r.d), rec.n);
+        V dir = reflected + m.fuzz * in_unit_sphere(g, k);
+        sc.d = dir;
+        att = mk(m.albedo[0], m.albedo[1], m.albedo[2]);
+        return dot(dir, rec.n) > 0.0f;
+    }
+    if (m.kind == rtdev::kMatDielectric) {  // dialectric.rs:32-61
+        att = mk(1.0f, 1.0f, 1.0f);
+        float ratio = rec.front ? 1.0f / m.ior : m.ior;
+        V ud = normalize(r.d);
+        float cos_t = rs_min(dot(-ud, rec.n), 1.0f);
+        float sin_t = __builtin_sqrtf(1.0f - cos_t * cos_t);
+        bool cannot = ratio * sin_t > 1.0f;
+        bool refl = cannot;
+        if (!cannot) {
+            float q = (1.0f - ratio) / (1.0f + ratio);  // Schlick, dialectric.rs:26-29
+            float r0 = q * q;
+            float x = 1.0f - cos_t;
+            float x2 = x * x;
+            float refl_p = r0 + (1.0f - r0) * (x * (x2 * x2));
+            refl = refl_p > std01(g, k);
+        }
+        sc.d = refl ? reflect(ud, rec.n) : refract(ud, rec.n, ratio);
+        return true;
+    }
+    if (m.kind == rtdev::kMatIsotropic) {  // isotropic.rs:31-43
+        sc.d = in_unit_sphere(g, k);
+        att = tex_value(S, m.tex, rec.u, rec.v, rec.p);
+        return true;
+    }
+    return false;  // DiffuseLight never scatters (diffuse_light.rs:26-32)
+}
+
+// ---------------------------------------------------------------------------
+// the kernel
+// ---------------------------------------------------------------------------
+RT_DEV void start_sample(const DevCamera& C, const DevParams& P, const Key& k, uint32_t x, uint32_t y,
+                         uint32_t pixel, uint32_t s, Rng& g, Ray& ray) {
+    g.sample = P.sample_base + s;
+    g.pixel = pixel;
+    g.block = 0u;
+    g.n = 0u;
+    // renderer.rs:141-142
+    float u = ((float)x + std01(g, k)) / (float)(P.width - 1u);
+    float v = ((float)y + std01(g, k)) / (float)(P.height - 1u);
+    // camera.rs:96-106
+    V rd = C.lens_radius * in_unit_disk(g, k);
+    V cu = mk(C.u[0], C.u[1], C.u[2]), cv = mk(C.v[0], C.v[1], C.v[2]);
+    V org = mk(C.origin[0], C.origin[1], C.origin[2]);
+    V offset = rd.x * cu + rd.y * cv;
+    ray.o = org + offset;
+    V llc = mk(C.llc[0], C.llc[1], C.llc[2]);
+    V hor = mk(C.horizontal[0], C.horizontal[1], C.horizontal[2]);
+    V ver = mk(C.vertical[0], C.vertical[1], C.vertical[2]);
+    ray.d = llc + u * hor + v * ver - org - offset;
+    float v01 = from_1_2(next_u32(g, k)) - 1.0f;  // gen_range(t0..=t1)
+    ray.time = v01 * C.time_scale + C.time_low;
+}
+
+__global__ __launch_bounds__(64) void render_blocks(DevScene S, DevCamera C, DevParams P, float* __restrict__ out,
+                                                     unsigned long long* __restrict__ seg_counter) {
+    extern __shared__ uint32_t lds_stack[];
+    const uint32_t lane = threadIdx.x;
+    uint32_t* stk = lds_stack + lane;
+    const uint32_t blk = P.shard_index + blockIdx.x * P.shard_count;
+    const uint32_t bx = blk % P.blocks_x, by = blk / P.blocks_x;
+    const uint32_t x = bx * 8u + (lane & 7u), y = by * 8u + (lane >> 3);
+    const bool valid = blk < P.num_blocks && x < P.width && y < P.height;
+    const Key k{P.seed_lo, P.seed_hi};
+    const bool exact = (P.flags & RT_FLAG_EXACT_BVH) != 0u;
+    const V bg = mk(P.bg[0], P.bg[1], P.bg[2]);
+    uint32_t nseg = 0;
+    if (valid) {
+        const uint32_t pixel = y * P.width + x;
+        V acc = mk(0.0f, 0.0f, 0.0f);
+        V L = mk(0.0f, 0.0f, 0.0f), T = mk(1.0f, 1.0f, 1.0f);
+        Rng g;
+        Ray ray;
+        uint32_t s = 0, depth = P.max_depth;
+        start_sample(C, P, k, x, y, pixel, s, g, ray);
+        for (;;) {
+            bool done;
+            if (depth == 0u) {
+                done = true;  // ray.rs:39-41
+            } else {
+                nseg += 1u;
+                float t;
+                uint32_t entry = 0, code = 0;
+                if (!world_hit(S, ray, g, k, t, entry, code, stk, exact)) {
+                    L = L + T * bg;
+                    done = true;
+                } else {
+                    Rec rec;
+                    make_record(S, entry, code, t, ray, rec);
+                    const DevMaterial m = S.mats[rec.mat];
+                    V e = m.kind == rtdev::kMatLight ? tex_value(S, m.tex, rec.u, rec.v, rec.p) : mk(0.0f, 0.0f, 0.0f);
+                    L = L + T * e;
+                    V att;
+                    Ray sc;
+                    if (scatter(S, m, ray, rec, g, k, att, sc)) {
+                        T = T * att;
+                        ray = sc;
+                        depth -= 1u;
+                        done = depth == 0u;
+                    } else {
+                        done = true;
+                    }
+                }
+            }
+            if (done) {
+                acc = acc + L;
+                s += 1u;
+                if (s >= P.spp) break;
+                L = mk(0.0f, 0.0f, 0.0f);
+                T = mk(1.0f, 1.0f, 1.0f);
+                depth = P.max_depth;
+                start_sample(C, P, k, x, y, pixel, s, g, ray);
+            }
+        }
+        V col = divs(acc, (float)P.spp);  // renderer.rs:147
+        float* o = out + (size_t)pixel * 3u;
+        o[0] = col.x;
+        o[1] = col.y;
+        o[2] = col.z;
+    }
+    if (seg_counter) {
+        unsigned long long v = nseg;
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+        if (lane == 0u) atomicAdd(seg_counter, v);
+    }
+}
+
+// Device numeric self-check (rt_device_numeric_eval).
+__global__ void numeric_eval(int op, const double* a, const double* b, double* out, uint32_t n) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    double x = a[i], y = b ? b[i] : 0.0;
+    double r = 0.0;
+    switch (op) {
+        case 0: r = __builtin_sqrt(x); break;
+        case 1: r = (double)__builtin_sqrtf((float)x); break;
+        case 2: r = (double)((float)x / (float)y); break;
+        case 3: r = (double)rt_sinf((float)x); break;
+        case 4: r = (double)rt_acosf((float)x); break;
+        case 5: r = (double)rt_atan2f((float)x, (float)y); break;
+        case 6: r = (double)rt_logf((float)x); break;
+        case 7: r = x / y; break;
+        default: r = 0.0; break;
+    }
+    out[i] = r;
+}
+
+}  // namespace
+
+// ===========================================================================
+// C ABI (device half)
+// ===========================================================================
+struct rt_scene {
+    int device = 0;
+    void* pool = nullptr;
+    uint64_t pool_bytes = 0;
+    DevScene dev{};
+    uint64_t counts[10] = {};
+};
+
+namespace {
+
+int hip_fail(hipError_t e, const char* what) {
+    return rthost::set_error(RT_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+struct DeviceGuard {  // restores the caller's current device (e.g. torch's)
+    int prev = -1;
+    bool ok = false;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        ok = hipSetDevice(dev) == hipSuccess;
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+int check_device(int device) {
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n == 0)
+        return rthost::set_error(RT_ERR_NO_DEVICE, "no HIP device visible (the device path has no CPU fallback)");
+    if (device < 0 || device >= n) return rthost::set_error(RT_ERR_INVALID, "device index out of range");
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return rthost::set_error(RT_ERR_NO_DEVICE, "device query failed");
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return rthost::set_error(RT_ERR_NO_DEVICE, std::string("device is ") + prop.gcnArchName +
+                                                       "; this build targets gfx950 (MI355X) only");
+    return RT_OK;
+}
+
+int check_params(const rt_render_params* p) {
+    if (!p) return rthost::set_error(RT_ERR_INVALID, "params is NULL");
+    if (p->width == 0 || p->height == 0) return rthost::set_error(RT_ERR_INVALID, "empty image");
+    if (p->samples_per_pixel == 0) return rthost::set_error(RT_ERR_INVALID, "samples_per_pixel must be > 0");
+    if (p->tile_width == 0 || p->tile_height == 0) return rthost::set_error(RT_ERR_INVALID, "tile size must be >= 1");
+    if (p->shard_count > 1 && p->shard_index >= p->shard_count)
+        return rthost::set_error(RT_ERR_INVALID, "shard_index >= shard_count");
+    if ((uint64_t)p->width * p->height > 0x7fffffffull) return rthost::set_error(RT_ERR_INVALID, "image too large");
+    return RT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rt_device_count(int* count) {
+    rthost::clear_error();
+    if (!count) return rthost::set_error(RT_ERR_INVALID, "count is NULL");
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    *count = n;
+    return RT_OK;
+}
+
+int rt_scene_upload(const rt_scene_desc* desc, int device, rt_scene_handle* out) {
+    rthost::clear_error();
+    if (!out) return rthost::set_error(RT_ERR_INVALID, "out is NULL");
+    *out = nullptr;
+    rthost::HostScene hs;
+    std::string err;
+    int rc = rthost::lower_scene(desc, &hs, &err);  // validate the IR before touching a device
+    if (rc) return rthost::set_error(rc, err);
+    if (hs.max_bvh_depth + 1 > 64) return rthost::set_error(RT_ERR_UNSUPPORTED, "BVH deeper than 64 levels");
+    if ((rc = check_device(device))) return rc;
+    struct Part {
+        const void* src;
+        uint64_t bytes;
+        uint64_t off;
+    };
+    std::vector<Part> parts = {
+        {hs.entries.data(), hs.entries.size() * sizeof(DevEntry), 0},
+        {hs.sph.data(), hs.sph.size() * sizeof(f4), 0},
+        {hs.sph_mat.data(), hs.sph_mat.size() * sizeof(uint32_t), 0},
+        {hs.msph.data(), hs.msph.size() * sizeof(f4), 0},
+        {hs.rect.data(), hs.rect.size() * sizeof(f4), 0},
+        {hs.tri.data(), hs.tri.size() * sizeof(f4), 0},
+        {hs.nodes.data(), hs.nodes.size() * sizeof(f4), 0},
+        {hs.mats.data(), hs.mats.size() * sizeof(DevMaterial), 0},
+        {hs.texs.data(), hs.texs.size() * sizeof(DevTexture), 0},
+        {hs.perm.data(), hs.perm.size(), 0},
+        {hs.texels.data(), hs.texels.size(), 0},
+    };
+    uint64_t total = 0;
+    for (auto& p : parts) {
+        p.off = total;
+        total += (p.bytes + 255u) & ~255ull;
+    }
+    if (total == 0) total = 256;
+    rt_scene* s = new (std::nothrow) rt_scene();
+    if (!s) return rthost::set_error(RT_ERR_OOM, "host allocation failed");
+    s->device = device;
+    {
+        DeviceGuard g(device);
+        hipError_t e = hipMalloc(&s->pool, total);
+        if (e != hipSuccess) {
+            delete s;
+            return rthost::set_error(RT_ERR_OOM, std::string("hipMalloc scene: ") + hipGetErrorString(e));
+        }
+        std::vector<uint8_t> staging(total, 0);
+        for (auto& p : parts)
+            if (p.bytes) memcpy(staging.data() + p.off, p.src, p.bytes);
+        e = hipMemcpy(s->pool, staging.data(), total, hipMemcpyHostToDevice);
+        if (e != hipSuccess) {
+            (void)hipFree(s->pool);
+            delete s;
+            return hip_fail(e, "hipMemcpy scene");
+        }
+    }
+    uint8_t* base = (uint8_t*)s->pool;
+    s->pool_bytes = total;
+    DevScene& d = s->dev;
+    d.entries = (const DevEntry*)(base + parts[0].off);
+    d.sph = (const f4*)(base + parts[1].off);
+    d.sph_mat = (const uint32_t*)(base + parts[2].off);
+    d.msph = (const f4*)(base + parts[3].off);
+    d.rect = (const f4*)(base + parts[4].off);
+    d.tri = (const f4*)(base + parts[5].off);
+    d.nodes = (const f4*)(base + parts[6].off);
+    d.mats = (const DevMaterial*)(base + parts[7].off);
+    d.texs = (const DevTexture*)(base + parts[8].off);
+    d.perm = base + parts[9].off;
+    d.texels = base + parts[10].off;
+    d.num_top = hs.num_top;
+    d.num_entries = (uint32_t)hs.entries.size();
+    d.stack_depth = hs.max_bvh_depth + 1u;
+    uint64_t c[10] = {hs.entries.size(), hs.sph.size(), hs.msph.size() / 3, hs.rect.size() / 2, hs.tri.size() / 3,
+                      hs.nodes.size() / 2, hs.mats.size(), hs.texs.size(), hs.max_bvh_depth, total};
+    memcpy(s->counts, c, sizeof c);
+    *out = s;
+    return RT_OK;
+}
+
+int rt_scene_free(rt_scene_handle s) {
+    rthost::clear_error();
+    if (!s) return RT_OK;
+    {
+        DeviceGuard g(s->device);
+        if (s->pool) (void)hipFree(s->pool);
+    }
+    delete s;
+    return RT_OK;
+}
+
+int rt_scene_info(rt_scene_handle s, uint64_t counts[10]) {
+    rthost::clear_error();
+    if (!s || !counts) return rthost::set_error(RT_ERR_INVALID, "NULL argument");
+    memcpy(counts, s->counts, sizeof s->counts);
+    return RT_OK;
+}
+
+int rt_render_launch(rt_scene_handle s, const rt_camera_desc* camera, const rt_render_params* p, float* d_out,
+                     unsigned long long* d_segments, void* stream) {
+    rthost::clear_error();
+    if (!s || !camera || !d_out) return rthost::set_error(RT_ERR_INVALID, "NULL scene/camera/output");
+    int rc = check_params(p);
+    if (rc) return rc;
+    DevCamera cam;
+    std::string err;
+    if ((rc = rthost::camera_basis(camera, &cam, &err))) return rthost::set_error(rc, err);
+    DevParams dp;
+    memset(&dp, 0, sizeof dp);
+    dp.width = p->width;
+    dp.height = p->height;
+    dp.spp = p->samples_per_pixel;
+    dp.max_depth = p->max_depth;
+    dp.seed_lo = (uint32_t)p->seed;
+    dp.seed_hi = (uint32_t)(p->seed >> 32);
+    dp.sample_base = p->sample_base;
+    dp.shard_count = p->shard_count > 1 ? p->shard_count : 1u;
+    dp.shard_index = p->shard_count > 1 ? p->shard_index : 0u;
+    dp.blocks_x = (p->width + 7u) / 8u;
+    dp.num_blocks = dp.blocks_x * ((p->height + 7u) / 8u);
+    dp.flags = p->flags;
+    dp.bg[0] = p->background[0];
+    dp.bg[1] = p->background[1];
+    dp.bg[2] = p->background[2];
+    uint32_t nblk = dp.num_blocks > dp.shard_index ? (dp.num_blocks - dp.shard_index + dp.shard_count - 1u) / dp.shard_count : 0u;
+    if (nblk == 0) return RT_OK;
+    size_t lds = (size_t)s->dev.stack_depth * 64u * sizeof(uint32_t);
+    DeviceGuard g(s->device);
+    if (!g.ok) return rthost::set_error(RT_ERR_HIP, "hipSetDevice failed");
+    hipLaunchKernelGGL(render_blocks, dim3(nblk), dim3(64), lds, (hipStream_t)stream, s->dev, cam, dp, d_out,
+                       d_segments);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(e, "render_blocks launch");
+    return RT_OK;
+}
+
+int rt_render(rt_scene_handle s, const rt_camera_desc* camera, const rt_render_params* p, float* host_out,
+              rt_stats* stats) {
+    rthost::clear_error();
+    if (!s || !camera || !host_out) return rthost::set_error(RT_ERR_INVALID, "NULL scene/camera/output");
+    int rc = check_params(p);
+    if (rc) return rc;
+    DeviceGuard g(s->device);
+    if (!g.ok) return rthost::set_error(RT_ERR_HIP, "hipSetDevice failed");
+    size_t bytes = (size_t)p->width * p->height * 3u * sizeof(float);
+    float* d_out = nullptr;
+    unsigned long long* d_seg = nullptr;
+    hipStream_t st = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    hipError_t e;
+    auto cleanup = [&]() {
+        if (e0) (void)hipEventDestroy(e0);
+        if (e1) (void)hipEventDestroy(e1);
+        if (st) (void)hipStreamDestroy(st);
+        if (d_out) (void)hipFree(d_out);
+        if (d_seg) (void)hipFree(d_seg);
+    };
+    if ((e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking)) != hipSuccess) { cleanup(); return hip_fail(e, "hipStreamCreate"); }
+    if ((e = hipMalloc(&d_out, bytes)) != hipSuccess) { cleanup(); return rthost::set_error(RT_ERR_OOM, "hipMalloc image"); }
+    if ((e = hipMalloc(&d_seg, sizeof(unsigned long long))) != hipSuccess) { cleanup(); return rthost::set_error(RT_ERR_OOM, "hipMalloc counter"); }
+    if ((e = hipMemcpyAsync(d_out, host_out, bytes, hipMemcpyHostToDevice, st)) != hipSuccess) { cleanup(); return hip_fail(e, "H2D image"); }
+    if ((e = hipMemsetAsync(d_seg, 0, sizeof(unsigned long long), st)) != hipSuccess) { cleanup(); return hip_fail(e, "memset"); }
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    (void)hipEventRecord(e0, st);
+    rc = rt_render_launch(s, camera, p, d_out, d_seg, st);
+    if (rc) { cleanup(); return rc; }
+    (void)hipEventRecord(e1, st);
+    unsigned long long seg = 0;
+    if ((e = hipMemcpyAsync(host_out, d_out, bytes, hipMemcpyDeviceToHost, st)) != hipSuccess) { cleanup(); return hip_fail(e, "D2H image"); }
+    if ((e = hipMemcpyAsync(&seg, d_seg, sizeof seg, hipMemcpyDeviceToHost, st)) != hipSuccess) { cleanup(); return hip_fail(e, "D2H counter"); }
+    if ((e = hipStreamSynchronize(st)) != hipSuccess) { cleanup(); return hip_fail(e, "render"); }
+    if (stats) {
+        float ms = 0.0f;
+        (void)hipEventElapsedTime(&ms, e0, e1);
+        uint64_t pixels = 0;
+        uint32_t sc = p->shard_count > 1 ? p->shard_count : 1u, si = p->shard_count > 1 ? p->shard_index : 0u;
+        uint32_t bxn = (p->width + 7u) / 8u;
+        for (uint32_t y = 0; y < p->height; ++y)
+            for (uint32_t x = 0; x < p->width; ++x)
+                if (((y / 8u) * bxn + x / 8u) % sc == si) pixels++;
+        stats->segments = seg;
+        stats->samples = pixels * p->samples_per_pixel;
+        stats->kernel_ms = ms;
+    }
+    cleanup();
+    return RT_OK;
+}
+
+int rt_device_numeric_eval(int op, const double* a, const double* b, double* out, uint32_t n) {
+    rthost::clear_error();
+    if (!a || !out) return rthost::set_error(RT_ERR_INVALID, "NULL argument");
+    int rc = check_device(0);
+    if (rc) return rc;
+    if (n == 0) return RT_OK;
+    DeviceGuard g(0);
+    double *da = nullptr, *db = nullptr, *dout = nullptr;
+    size_t bytes = (size_t)n * sizeof(double);
+    hipError_t e = hipMalloc(&da, bytes);
+    if (e == hipSuccess && b) e = hipMalloc(&db, bytes);
+    if (e == hipSuccess) e = hipMalloc(&dout, bytes);
+    if (e == hipSuccess) e = hipMemcpy(da, a, bytes, hipMemcpyHostToDevice);
+    if (e == hipSuccess && b) e = hipMemcpy(db, b, bytes, hipMemcpyHostToDevice);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(numeric_eval, dim3((n + 255u) / 256u), dim3(256), 0, nullptr, op, da, db, dout, n);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpy(out, dout, bytes, hipMemcpyDeviceToHost);
+    if (da) (void)hipFree(da);
+    if (db) (void)hipFree(db);
+    if (dout) (void)hipFree(dout);
+    if (e != hipSuccess) return hip_fail(e, "numeric_eval");
+    return RT_OK;
+}
+
+}  // extern "C"

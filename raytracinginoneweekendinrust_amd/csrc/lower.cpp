@@ -1,0 +1,629 @@
+// lower.cpp — scene IR -> device SoA layout (see device_scene.hpp).
+//
+// Host-side construction work the reference does in its constructors:
+//   Bvh::new / BvhNode::new_helper   src/bvh.rs:46-62, 249-333 (random split axis,
+//                                    stable sort on bounding_box(0,0).min[axis],
+//                                    median split, 1- and 2-object leaves)
+//   Hittable::bounding_box           per primitive file, cited below
+//   Cube::new                        src/geometry/cube.rs:23-81 (six rects, fixed order)
+//   RotateY::new                     src/geometry/instance.rs:63-67 (sin / cos)
+//   ConstantMedium::new              src/hittable.rs:150-174 (-1 / density)
+//   Metal::new                       src/materials/metal.rs:17-22 (fuzz clamp)
+//   Perlin::new                      noise 0.8.2 PermutationTable (marble.rs:14)
+//   Camera::new                      src/camera.rs:44-81
+#include "lower.hpp"
+
+#include <string.h>
+
+#include <algorithm>
+#include <functional>
+#include <unordered_map>
+
+#include "../../include/rt_numeric_spec.h"
+
+namespace rthost {
+
+using rtdev::f4;
+
+uint64_t HostScene::bytes() const {
+    return entries.size() * sizeof(rtdev::DevEntry) + sph.size() * 16 + sph_mat.size() * 4 +
+           msph.size() * 16 + rect.size() * 16 + tri.size() * 16 + nodes.size() * 16 +
+           mats.size() * sizeof(rtdev::DevMaterial) + texs.size() * sizeof(rtdev::DevTexture) +
+           perm.size() + texels.size();
+}
+
+// ---------------------------------------------------------------------------
+// small f32 vector helpers (glam 0.22 evaluation order)
+// ---------------------------------------------------------------------------
+namespace {
+struct V {
+    float x, y, z;
+};
+inline V vadd(V a, V b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+inline V vsub(V a, V b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+inline V vscale(float s, V a) { return {s * a.x, s * a.y, s * a.z}; }
+inline V vdivs(V a, float s) { return {a.x / s, a.y / s, a.z / s}; }
+inline float vdot(V a, V b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
+inline V vcross(V a, V b) { return {a.y * b.z - b.y * a.z, a.z * b.x - b.z * a.x, a.x * b.y - b.x * a.y}; }
+inline V vnorm(V a) {
+    float r = 1.0f / __builtin_sqrtf(vdot(a, a));
+    return {a.x * r, a.y * r, a.z * r};
+}
+inline float rs_min(float a, float b) {
+    if (a != a) return b;
+    if (b != b) return a;
+    return a < b ? a : b;
+}
+inline float rs_max(float a, float b) {
+    if (a != a) return b;
+    if (b != b) return a;
+    return a > b ? a : b;
+}
+inline float rs_clamp(float x, float lo, float hi) {
+    if (x < lo) x = lo;
+    if (x > hi) x = hi;
+    return x;
+}
+struct Box {
+    V mn, mx;
+};
+inline Box box_union(const Box& a, const Box& b) {  // aabb.rs:43-62
+    return {{rs_min(a.mn.x, b.mn.x), rs_min(a.mn.y, b.mn.y), rs_min(a.mn.z, b.mn.z)},
+            {rs_max(a.mx.x, b.mx.x), rs_max(a.mx.y, b.mx.y), rs_max(a.mx.z, b.mx.z)}};
+}
+inline int total_cmp(float a, float b) {  // f32::total_cmp
+    int32_t l = (int32_t)rt_spec_f32_bits(a), r = (int32_t)rt_spec_f32_bits(b);
+    l ^= (int32_t)(((uint32_t)(l >> 31)) >> 1);
+    r ^= (int32_t)(((uint32_t)(r >> 31)) >> 1);
+    return (l > r) - (l < r);
+}
+constexpr float kEps = 1.1920929e-07f;  // f32::EPSILON
+
+inline uint32_t fbits(float f) { return rt_spec_f32_bits(f); }
+inline float bitsf(uint32_t u) { return rt_spec_bits_f32(u); }
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// random streams shared with the oracle
+// ---------------------------------------------------------------------------
+void philox4x32_10(const uint32_t ctr_in[4], const uint32_t key_in[2], uint32_t out[4]) {
+    uint32_t c0 = ctr_in[0], c1 = ctr_in[1], c2 = ctr_in[2], c3 = ctr_in[3];
+    uint32_t k0 = key_in[0], k1 = key_in[1];
+    for (int r = 0; r < 10; ++r) {
+        if (r) {
+            k0 += 0x9E3779B9u;
+            k1 += 0xBB67AE85u;
+        }
+        uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
+        uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0, n1 = (uint32_t)p1;
+        uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1, n3 = (uint32_t)p0;
+        c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+    }
+    out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+namespace {
+// Split-axis stream of one Bvh::new: Philox key = IR seed, counter (block, 0, 0, 0);
+// rand 0.8.5 UniformInt::sample_single_inclusive(0, 2) (bvh.rs:255).
+struct AxisStream {
+    uint32_t key[2], block = 0, buf[4];
+    int idx = 4;
+    explicit AxisStream(uint64_t seed) {
+        key[0] = (uint32_t)seed;
+        key[1] = (uint32_t)(seed >> 32);
+    }
+    uint32_t next() {
+        if (idx == 4) {
+            uint32_t ctr[4] = {block++, 0u, 0u, 0u};
+            philox4x32_10(ctr, key, buf);
+            idx = 0;
+        }
+        return buf[idx++];
+    }
+    int axis() {
+        const uint32_t range = 3u, zone = (3u << 30) - 1u;
+        for (;;) {
+            uint64_t m = (uint64_t)next() * range;
+            if ((uint32_t)m <= zone) return (int)(m >> 32);
+        }
+    }
+};
+}  // namespace
+
+void perlin_permutation(uint32_t seed, uint8_t out[256]) {
+    uint32_t x = 1u, y = seed, z = seed, w = seed;  // XorShiftRng::from_seed([1, seed, seed, seed])
+    auto next = [&]() {
+        uint32_t t = x ^ (x << 11);
+        x = y; y = z; z = w;
+        w = w ^ (w >> 19) ^ (t ^ (t >> 8));
+        return w;
+    };
+    for (int i = 0; i < 256; ++i) out[i] = (uint8_t)i;
+    for (uint32_t i = 255; i >= 1; --i) {  // SliceRandom::shuffle (rand 0.7)
+        uint32_t n = i + 1, zone = (n << __builtin_clz(n)) - 1u, j;
+        for (;;) {
+            uint64_t m = (uint64_t)next() * n;
+            if ((uint32_t)m <= zone) {
+                j = (uint32_t)(m >> 32);
+                break;
+            }
+        }
+        std::swap(out[i], out[j]);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Camera::new
+// ---------------------------------------------------------------------------
+int camera_basis(const rt_camera_desc* d, rtdev::DevCamera* c, std::string* err) {
+    V lf{d->look_from[0], d->look_from[1], d->look_from[2]};
+    V la{d->look_at[0], d->look_at[1], d->look_at[2]};
+    V vup{d->view_up[0], d->view_up[1], d->view_up[2]};
+    float theta = rt_to_radians(d->vfov_deg);
+    float h = rt_tanf(theta / 2.0f);
+    float vh = 2.0f * h;
+    float vw = d->aspect_ratio * vh;
+    V w = vnorm(vsub(lf, la));
+    V u = vnorm(vcross(vup, w));
+    V v = vcross(w, u);
+    V hor = vscale(d->focus_dist * vw, u);
+    V ver = vscale(d->focus_dist * vh, v);
+    V llc = vsub(vsub(vsub(lf, vdivs(hor, 2.0f)), vdivs(ver, 2.0f)), vscale(d->focus_dist, w));
+    auto put = [](float* dst, V a) {
+        dst[0] = a.x;
+        dst[1] = a.y;
+        dst[2] = a.z;
+    };
+    put(c->origin, lf);
+    put(c->horizontal, hor);
+    put(c->vertical, ver);
+    put(c->llc, llc);
+    put(c->u, u);
+    put(c->v, v);
+    c->lens_radius = d->aperture / 2.0f;
+    c->time_low = d->time0;
+    // UniformFloat::new_inclusive (rand 0.8.5) for gen_range(time0..=time1), camera.rs:104
+    if (!(d->time0 <= d->time1)) {
+        *err = "Uniform::new_inclusive called with `low > high` (cam time0 > time1)";
+        return RT_ERR_INVALID;
+    }
+    const float max_rand = bitsf(0x3fffffffu | 0x3f800000u) - 1.0f;  // (u32::MAX >> 9) in [1,2) - 1
+    float scale = (d->time1 - d->time0) / max_rand;
+    while (scale * max_rand + d->time0 > d->time1) scale = bitsf(fbits(scale) - 1u);
+    c->time_scale = scale;
+    return RT_OK;
+}
+
+// ---------------------------------------------------------------------------
+// lowering
+// ---------------------------------------------------------------------------
+namespace {
+
+struct LeafInfo {
+    uint32_t code;
+    Box box01;  // bounding_box(time0, time1) of the BVH
+    float key[3];
+};
+
+class Lowerer {
+   public:
+    Lowerer(const rt_scene_desc* d, HostScene* out, std::string* err) : d_(d), s_(out), err_(err) {}
+
+    int run() {
+        if (!d_ || !d_->nodes || d_->num_nodes == 0) return fail(RT_ERR_INVALID, "empty scene");
+        if (d_->num_list_items && !d_->list_items) return fail(RT_ERR_INVALID, "list_items is NULL");
+        if (d_->world < 0 || (uint32_t)d_->world >= d_->num_nodes || d_->nodes[d_->world].kind != RT_OBJ_LIST)
+            return fail(RT_ERR_INVALID, "world must be a LIST node");
+        std::vector<rtdev::DevEntry> top;
+        Chain chain;
+        int rc = lower_entry(d_->world, chain, &top, 0);
+        if (rc) return rc;
+        s_->num_top = (uint32_t)top.size();
+        for (auto& e : top)
+            if (e.kind == rtdev::kEntMedium) e.payload += s_->num_top;
+        s_->entries = top;
+        s_->entries.insert(s_->entries.end(), aux_.begin(), aux_.end());
+        if (s_->entries.empty()) {
+            // An empty world: keep one inert entry so device pointers are valid.
+            s_->num_top = 0;
+        }
+        return RT_OK;
+    }
+
+   private:
+    struct Chain {
+        int n = 0;
+        f4 op[rtdev::kMaxTransforms];
+    };
+
+    int fail(int code, const std::string& m) {
+        *err_ = m;
+        return code;
+    }
+    const rt_node& node(int i) const { return d_->nodes[i]; }
+    bool valid(int i) const { return i >= 0 && (uint32_t)i < d_->num_nodes; }
+    int list_range(const rt_node& n, uint32_t* first, uint32_t* count) {
+        if (n.ref[0] < 0 || n.ref[1] < 0 || (uint64_t)n.ref[0] + (uint64_t)n.ref[1] > d_->num_list_items)
+            return fail(RT_ERR_INVALID, "LIST range out of bounds");
+        *first = (uint32_t)n.ref[0];
+        *count = (uint32_t)n.ref[1];
+        return RT_OK;
+    }
+
+    // --- textures / materials --------------------------------------------
+    int lower_texture(int idx, uint32_t* out, int depth) {
+        if (!valid(idx)) return fail(RT_ERR_INVALID, "texture ref out of range");
+        if (depth > 64) return fail(RT_ERR_INVALID, "texture graph too deep (cycle?)");
+        auto it = tex_memo_.find(idx);
+        if (it != tex_memo_.end()) {
+            *out = it->second;
+            return RT_OK;
+        }
+        const rt_node& n = node(idx);
+        rtdev::DevTexture t;
+        memset(&t, 0, sizeof t);
+        switch (n.kind) {
+            case RT_TEX_SOLID:  // solid_color.rs:21-25
+                t.kind = rtdev::kTexSolid;
+                t.color[0] = n.f[0]; t.color[1] = n.f[1]; t.color[2] = n.f[2];
+                break;
+            case RT_TEX_CHECKER: {  // checker.rs:27-37
+                uint32_t even, odd;
+                int rc = lower_texture(n.ref[0], &even, depth + 1);
+                if (rc) return rc;
+                if ((rc = lower_texture(n.ref[1], &odd, depth + 1))) return rc;
+                t.kind = rtdev::kTexChecker;
+                t.a = even;
+                t.b = odd;
+                t.scale = n.f[0];
+                break;
+            }
+            case RT_TEX_MARBLE: {  // marble.rs:13-20: Perlin(seed) + Turbulence distortion Fbm seeds 0..7
+                t.kind = rtdev::kTexMarble;
+                t.scale = n.f[0];
+                t.a = (uint32_t)(s_->perm.size() / 256);
+                uint8_t tab[256];
+                perlin_permutation((uint32_t)n.seed, tab);
+                s_->perm.insert(s_->perm.end(), tab, tab + 256);
+                for (uint32_t sd = 0; sd < 8; ++sd) {
+                    perlin_permutation(sd, tab);
+                    s_->perm.insert(s_->perm.end(), tab, tab + 256);
+                }
+                break;
+            }
+            case RT_TEX_IMAGE: {  // image_texture.rs:13-19 (decoded RGB8 supplied in the IR)
+                uint64_t w = (uint32_t)n.ref[0], h = (uint32_t)n.ref[1];
+                if (n.ref[0] <= 0 || n.ref[1] <= 0) return fail(RT_ERR_INVALID, "image texture with empty size");
+                uint64_t need = w * h * 3u;
+                if (!d_->image_data || n.seed + need > d_->image_bytes)
+                    return fail(RT_ERR_INVALID, "image texture texels out of bounds");
+                t.kind = rtdev::kTexImage;
+                t.a = (uint32_t)s_->texels.size();
+                t.b = (uint32_t)w;
+                t.c = (uint32_t)h;
+                if (s_->texels.size() + need > 0xffffffffull) return fail(RT_ERR_UNSUPPORTED, "texel pool > 4 GB");
+                s_->texels.insert(s_->texels.end(), d_->image_data + n.seed, d_->image_data + n.seed + need);
+                break;
+            }
+            default:
+                return fail(RT_ERR_INVALID, "node " + std::to_string(idx) + " is not a texture");
+        }
+        uint32_t id = (uint32_t)s_->texs.size();
+        s_->texs.push_back(t);
+        tex_memo_[idx] = id;
+        *out = id;
+        return RT_OK;
+    }
+
+    int lower_material(int idx, uint32_t* out) {
+        if (!valid(idx)) return fail(RT_ERR_INVALID, "material ref out of range");
+        auto it = mat_memo_.find(idx);
+        if (it != mat_memo_.end()) {
+            *out = it->second;
+            return RT_OK;
+        }
+        const rt_node& n = node(idx);
+        rtdev::DevMaterial m;
+        memset(&m, 0, sizeof m);
+        int rc = RT_OK;
+        switch (n.kind) {
+            case RT_MAT_LAMBERTIAN: m.kind = rtdev::kMatLambertian; rc = lower_texture(n.ref[0], &m.tex, 0); break;
+            case RT_MAT_DIFFUSE_LIGHT: m.kind = rtdev::kMatLight; rc = lower_texture(n.ref[0], &m.tex, 0); break;
+            case RT_MAT_ISOTROPIC: m.kind = rtdev::kMatIsotropic; rc = lower_texture(n.ref[0], &m.tex, 0); break;
+            case RT_MAT_METAL:
+                m.kind = rtdev::kMatMetal;
+                m.albedo[0] = n.f[0]; m.albedo[1] = n.f[1]; m.albedo[2] = n.f[2];
+                m.fuzz = rs_clamp(n.f[3], 0.0f, 1.0f);  // metal.rs:20
+                break;
+            case RT_MAT_DIELECTRIC: m.kind = rtdev::kMatDielectric; m.ior = n.f[0]; break;
+            default:
+                return fail(RT_ERR_INVALID, "node " + std::to_string(idx) + " is not a material");
+        }
+        if (rc) return rc;
+        uint32_t id = (uint32_t)s_->mats.size();
+        s_->mats.push_back(m);
+        mat_memo_[idx] = id;
+        *out = id;
+        return RT_OK;
+    }
+
+    uint32_t phase_material(uint32_t tex) {  // Isotropic::new(texture), hittable.rs:159
+        auto it = phase_memo_.find(tex);
+        if (it != phase_memo_.end()) return it->second;
+        rtdev::DevMaterial m;
+        memset(&m, 0, sizeof m);
+        m.kind = rtdev::kMatIsotropic;
+        m.tex = tex;
+        uint32_t id = (uint32_t)s_->mats.size();
+        s_->mats.push_back(m);
+        phase_memo_[tex] = id;
+        return id;
+    }
+
+    // --- primitives ------------------------------------------------------
+    static bool is_prim(uint32_t k) {
+        return k == RT_OBJ_SPHERE || k == RT_OBJ_MOVING_SPHERE || k == RT_OBJ_XY_RECT || k == RT_OBJ_XZ_RECT ||
+               k == RT_OBJ_YZ_RECT || k == RT_OBJ_CUBE || k == RT_OBJ_TRI;
+    }
+
+    uint32_t push_rect(uint32_t axis, float a0, float a1, float b0, float b1, float k, uint32_t mat) {
+        uint32_t id = (uint32_t)(s_->rect.size() / 2);
+        s_->rect.push_back({k, a0, a1, b0});
+        s_->rect.push_back({b1, bitsf(axis), bitsf(mat), 0.0f});
+        return id;
+    }
+
+    int lower_prim(int idx, uint32_t* code) {
+        auto it = prim_memo_.find(idx);
+        if (it != prim_memo_.end()) {
+            *code = it->second;
+            return RT_OK;
+        }
+        const rt_node& n = node(idx);
+        uint32_t mat;
+        int rc = lower_material(n.ref[0], &mat);
+        if (rc) return rc;
+        const float* f = n.f;
+        switch (n.kind) {
+            case RT_OBJ_SPHERE: {
+                uint32_t id = (uint32_t)s_->sph.size();
+                s_->sph.push_back({f[0], f[1], f[2], f[3]});
+                s_->sph_mat.push_back(mat);
+                *code = rtdev::leaf_code(rtdev::kLeafSphere, id);
+                break;
+            }
+            case RT_OBJ_MOVING_SPHERE: {
+                uint32_t id = (uint32_t)(s_->msph.size() / 3);
+                s_->msph.push_back({f[0], f[1], f[2], f[8]});
+                s_->msph.push_back({f[3] - f[0], f[4] - f[1], f[5] - f[2], f[6]});
+                s_->msph.push_back({f[7] - f[6], bitsf(mat), 0.0f, 0.0f});
+                *code = rtdev::leaf_code(rtdev::kLeafMSphere, id);
+                break;
+            }
+            case RT_OBJ_XY_RECT: *code = rtdev::leaf_code(rtdev::kLeafRect, push_rect(0, f[0], f[1], f[2], f[3], f[4], mat)); break;
+            case RT_OBJ_XZ_RECT: *code = rtdev::leaf_code(rtdev::kLeafRect, push_rect(1, f[0], f[1], f[2], f[3], f[4], mat)); break;
+            case RT_OBJ_YZ_RECT: *code = rtdev::leaf_code(rtdev::kLeafRect, push_rect(2, f[0], f[1], f[2], f[3], f[4], mat)); break;
+            case RT_OBJ_CUBE: {  // cube.rs:25-74
+                float x0 = f[0], y0 = f[1], z0 = f[2], x1 = f[3], y1 = f[4], z1 = f[5];
+                uint32_t first = push_rect(0, x0, x1, y0, y1, z0, mat);
+                push_rect(0, x0, x1, y0, y1, z1, mat);
+                push_rect(1, x0, x1, z0, z1, y0, mat);
+                push_rect(1, x0, x1, z0, z1, y1, mat);
+                push_rect(2, y0, y1, z0, z1, x0, mat);
+                push_rect(2, y0, y1, z0, z1, x1, mat);
+                *code = rtdev::leaf_code(rtdev::kLeafCube, first);
+                break;
+            }
+            case RT_OBJ_TRI: {
+                uint32_t id = (uint32_t)(s_->tri.size() / 3);
+                s_->tri.push_back({f[0], f[1], f[2], bitsf(mat)});
+                s_->tri.push_back({f[3] - f[0], f[4] - f[1], f[5] - f[2], 0.0f});
+                s_->tri.push_back({f[6] - f[0], f[7] - f[1], f[8] - f[2], 0.0f});
+                *code = rtdev::leaf_code(rtdev::kLeafTri, id);
+                break;
+            }
+            default:
+                return fail(RT_ERR_INVALID, "not a primitive");
+        }
+        if (rtdev::leaf_index(*code) > rtdev::kMaxIndex - 8) return fail(RT_ERR_UNSUPPORTED, "too many primitives");
+        prim_memo_[idx] = *code;
+        return RT_OK;
+    }
+
+    // Hittable::bounding_box(t0, t1) of a primitive node.
+    Box prim_box(const rt_node& n, float t0, float t1) {
+        const float* f = n.f;
+        switch (n.kind) {
+            case RT_OBJ_SPHERE: {  // sphere.rs:105-109
+                V c{f[0], f[1], f[2]}, r{f[3], f[3], f[3]};
+                return {vsub(c, r), vadd(c, r)};
+            }
+            case RT_OBJ_MOVING_SPHERE: {  // moving_sphere.rs:86-93 (end_box.min uses time_0)
+                V c0{f[0], f[1], f[2]}, c1{f[3], f[4], f[5]}, r{f[8], f[8], f[8]};
+                auto center = [&](float time) { return vadd(c0, vscale((time - f[6]) / (f[7] - f[6]), vsub(c1, c0))); };
+                Box sb{vsub(center(t0), r), vadd(center(t0), r)};
+                Box eb{vsub(center(t0), r), vadd(center(t1), r)};
+                return box_union(sb, eb);
+            }
+            case RT_OBJ_XY_RECT: return {{f[0], f[2], f[4] - kEps}, {f[1], f[3], f[4] + kEps}};  // rectangle.rs:67-73
+            case RT_OBJ_XZ_RECT: return {{f[0], f[4] - kEps, f[2]}, {f[1], f[4] + kEps, f[3]}};  // :129-135
+            case RT_OBJ_YZ_RECT: return {{f[4] - kEps, f[0], f[2]}, {f[4] + kEps, f[1], f[3]}};  // :191-197
+            case RT_OBJ_CUBE: return {{f[0], f[1], f[2]}, {f[3], f[4], f[5]}};                  // cube.rs:95-97
+            default: {                                                                         // triangle.rs:94-107
+                return {{rs_min(f[0], rs_min(f[3], f[6])) - kEps, rs_min(f[1], rs_min(f[4], f[7])) - kEps,
+                         rs_min(f[2], rs_min(f[5], f[8])) - kEps},
+                        {rs_max(f[0], rs_max(f[3], f[6])) + kEps, rs_max(f[1], rs_max(f[4], f[7])) + kEps,
+                         rs_max(f[2], rs_max(f[5], f[8])) + kEps}};
+            }
+        }
+    }
+
+    // --- BVH ---------------------------------------------------------------
+    struct TNode {
+        uint32_t child[2];  // temp node index or leaf code
+        bool is_node[2];
+        Box box;
+    };
+
+    int bvh_build(const rt_node& n, uint32_t* root_out) {
+        uint32_t first, count;
+        if (!valid(n.ref[0]) || node(n.ref[0]).kind != RT_OBJ_LIST) return fail(RT_ERR_INVALID, "BVH must reference a LIST");
+        int rc = list_range(node(n.ref[0]), &first, &count);
+        if (rc) return rc;
+        if (count == 0) return fail(RT_ERR_INVALID, "BVH over an empty list");
+        std::vector<LeafInfo> items(count);
+        for (uint32_t i = 0; i < count; ++i) {
+            int ni = d_->list_items[first + i];
+            if (!valid(ni)) return fail(RT_ERR_INVALID, "list item out of range");
+            const rt_node& c = node(ni);
+            if (!is_prim(c.kind))
+                return fail(RT_ERR_UNSUPPORTED, "device BVH leaves must be Sphere/MovingSphere/Rect/Cube/Tri (node " +
+                                                    std::to_string(ni) + " kind " + std::to_string(c.kind) + ")");
+            if ((rc = lower_prim(ni, &items[i].code))) return rc;
+            items[i].box01 = prim_box(c, n.f[0], n.f[1]);
+            Box b00 = prim_box(c, 0.0f, 0.0f);  // box_compare uses bounding_box(0.0, 0.0), bvh.rs:421-422
+            items[i].key[0] = b00.mn.x;
+            items[i].key[1] = b00.mn.y;
+            items[i].key[2] = b00.mn.z;
+        }
+        std::vector<TNode> tn;
+        tn.reserve(count * 2 + 1);
+        AxisStream ax(n.seed);
+        std::vector<LeafInfo> tmp(count);
+        // BvhNode::new_helper, bvh.rs:249-333; returns the temp node index.
+        std::function<uint32_t(LeafInfo*, uint32_t, uint32_t)> helper = [&](LeafInfo* o, uint32_t cnt,
+                                                                            uint32_t depth) -> uint32_t {
+            if (depth > max_depth_) max_depth_ = depth;
+            int axis = ax.axis();
+            TNode t;
+            if (cnt == 1) {
+                t.child[0] = o[0].code;
+                t.is_node[0] = false;
+                t.child[1] = rtdev::kChildEmpty;  // same object twice in the reference: tested once here
+                t.is_node[1] = false;
+                t.box = box_union(o[0].box01, o[0].box01);
+            } else if (cnt == 2) {
+                int a = total_cmp(o[0].key[axis], o[1].key[axis]) < 0 ? 0 : 1;
+                t.child[0] = o[a].code;
+                t.child[1] = o[1 - a].code;
+                t.is_node[0] = t.is_node[1] = false;
+                t.box = box_union(o[a].box01, o[1 - a].box01);
+            } else {
+                std::stable_sort(o, o + cnt, [axis](const LeafInfo& p, const LeafInfo& q) {
+                    return total_cmp(p.key[axis], q.key[axis]) < 0;
+                });
+                uint32_t mid = cnt / 2;
+                uint32_t l = helper(o, mid, depth + 1);
+                uint32_t r = helper(o + mid, cnt - mid, depth + 1);
+                t.child[0] = l;
+                t.child[1] = r;
+                t.is_node[0] = t.is_node[1] = true;
+                t.box = box_union(tn[l].box, tn[r].box);
+            }
+            tn.push_back(t);
+            return (uint32_t)tn.size() - 1;
+        };
+        uint32_t troot = helper(items.data(), count, 1);
+        // Flatten in DFS preorder.
+        uint32_t base = (uint32_t)(s_->nodes.size() / 2);
+        std::vector<uint32_t> remap(tn.size());
+        uint32_t next = base;
+        std::function<void(uint32_t)> order = [&](uint32_t i) {
+            remap[i] = next++;
+            for (int k = 0; k < 2; ++k)
+                if (tn[i].is_node[k]) order(tn[i].child[k]);
+        };
+        order(troot);
+        if (next > rtdev::kMaxIndex) return fail(RT_ERR_UNSUPPORTED, "too many BVH nodes");
+        s_->nodes.resize((size_t)next * 2);
+        for (uint32_t i = 0; i < tn.size(); ++i) {
+            uint32_t o = remap[i];
+            uint32_t l = tn[i].is_node[0] ? remap[tn[i].child[0]] : tn[i].child[0];
+            uint32_t r = tn[i].is_node[1] ? remap[tn[i].child[1]] : tn[i].child[1];
+            s_->nodes[2 * o] = {tn[i].box.mn.x, tn[i].box.mn.y, tn[i].box.mn.z, bitsf(l)};
+            s_->nodes[2 * o + 1] = {tn[i].box.mx.x, tn[i].box.mx.y, tn[i].box.mx.z, bitsf(r)};
+        }
+        s_->max_bvh_depth = std::max(s_->max_bvh_depth, max_depth_);
+        *root_out = remap[troot];
+        return RT_OK;
+    }
+
+    // --- entries -----------------------------------------------------------
+    int lower_entry(int idx, Chain chain, std::vector<rtdev::DevEntry>* out, int depth) {
+        if (!valid(idx)) return fail(RT_ERR_INVALID, "hittable ref out of range");
+        if (depth > 256) return fail(RT_ERR_INVALID, "hittable graph too deep (cycle?)");
+        const rt_node& n = node(idx);
+        rtdev::DevEntry e;
+        memset(&e, 0, sizeof e);
+        e.ntf = (uint32_t)chain.n;
+        for (int i = 0; i < chain.n; ++i) e.tf[i] = chain.op[i];
+        int rc;
+        switch (n.kind) {
+            case RT_OBJ_LIST: {  // hittable.rs:100-118 — flattening keeps order and closest_so_far
+                uint32_t first, count;
+                if ((rc = list_range(n, &first, &count))) return rc;
+                for (uint32_t i = 0; i < count; ++i)
+                    if ((rc = lower_entry(d_->list_items[first + i], chain, out, depth + 1))) return rc;
+                return RT_OK;
+            }
+            case RT_OBJ_TRANSLATE:
+            case RT_OBJ_ROTATE_Y: {
+                if (chain.n == rtdev::kMaxTransforms)
+                    return fail(RT_ERR_UNSUPPORTED, "more than 3 nested Translate/RotateY");
+                Chain c2 = chain;
+                if (n.kind == RT_OBJ_TRANSLATE) {
+                    c2.op[c2.n++] = {n.f[0], n.f[1], n.f[2], 0.0f};
+                } else {
+                    float radians = rt_to_radians(n.f[0]);  // instance.rs:64-67
+                    c2.op[c2.n++] = {rt_sinf(radians), rt_cosf(radians), 0.0f, 1.0f};
+                }
+                return lower_entry(n.ref[0], c2, out, depth + 1);
+            }
+            case RT_OBJ_BVH:
+                e.kind = rtdev::kEntBvh;
+                if ((rc = bvh_build(n, &e.payload))) return rc;
+                out->push_back(e);
+                return RT_OK;
+            case RT_OBJ_CONSTANT_MEDIUM: {  // hittable.rs:150-174
+                std::vector<rtdev::DevEntry> b;
+                Chain none;
+                if ((rc = lower_entry(n.ref[0], none, &b, depth + 1))) return rc;
+                if (b.size() != 1 || b[0].kind == rtdev::kEntMedium)
+                    return fail(RT_ERR_UNSUPPORTED, "ConstantMedium boundary must be one primitive/cube/BVH (optionally "
+                                                    "under Translate/RotateY)");
+                uint32_t tex;
+                if ((rc = lower_texture(n.ref[1], &tex, 0))) return rc;
+                e.kind = rtdev::kEntMedium;
+                e.payload = (uint32_t)aux_.size();  // fixed up by num_top in run()
+                e.phase_mat = phase_material(tex);
+                e.neg_inv_density = -1.0f / n.f[0];
+                aux_.push_back(b[0]);
+                out->push_back(e);
+                return RT_OK;
+            }
+            default:
+                if (!is_prim(n.kind)) return fail(RT_ERR_INVALID, "node " + std::to_string(idx) + " is not a hittable");
+                e.kind = rtdev::kEntGeom;
+                if ((rc = lower_prim(idx, &e.payload))) return rc;
+                out->push_back(e);
+                return RT_OK;
+        }
+    }
+
+    const rt_scene_desc* d_;
+    HostScene* s_;
+    std::string* err_;
+    std::vector<rtdev::DevEntry> aux_;
+    std::unordered_map<int, uint32_t> tex_memo_, mat_memo_, prim_memo_, phase_memo_;
+    uint32_t max_depth_ = 0;
+};
+
+}  // namespace
+
+int lower_scene(const rt_scene_desc* desc, HostScene* out, std::string* err) {
+    *out = HostScene();
+    Lowerer l(desc, out, err);
+    return l.run();
+}
+
+}  // namespace rthost

@@ -1,0 +1,41 @@
+// lower.hpp — host-side lowering of the scene IR (include/rt.h) to the device
+// layout (device_scene.hpp), plus the host halves of Camera::new and the
+// split-axis / Perlin random streams that must match the oracle bit for bit.
+#pragma once
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/rt.h"
+#include "device_scene.hpp"
+
+namespace rthost {
+
+struct HostScene {
+    std::vector<rtdev::DevEntry> entries;
+    uint32_t num_top = 0;
+    std::vector<rtdev::f4> sph;
+    std::vector<uint32_t> sph_mat;
+    std::vector<rtdev::f4> msph, rect, tri, nodes;
+    std::vector<rtdev::DevMaterial> mats;
+    std::vector<rtdev::DevTexture> texs;
+    std::vector<uint8_t> perm, texels;
+    uint32_t max_bvh_depth = 0;  // internal levels of the deepest BVH
+    uint64_t bytes() const;
+};
+
+// Returns RT_OK or a negative rt_status with a message in *err.
+int lower_scene(const rt_scene_desc* desc, HostScene* out, std::string* err);
+
+// Camera::new (src/camera.rs:44-81); returns RT_ERR_INVALID when time0 > time1
+// (the reference panics in UniformFloat::new_inclusive).
+int camera_basis(const rt_camera_desc* cam, rtdev::DevCamera* out, std::string* err);
+
+// Philox4x32-10 (Random123), host copy used by the split-axis stream.
+void philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
+
+// noise 0.8.2 PermutationTable::new(seed) restatement (XorShift128 + rand 0.7 shuffle).
+void perlin_permutation(uint32_t seed, uint8_t out[256]);
+
+}  // namespace rthost

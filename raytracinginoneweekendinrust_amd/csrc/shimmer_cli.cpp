@@ -1,0 +1,213 @@
+// shimmer_cli.cpp — command-line drop-in for the reference binary (src/main.rs:35-183).
+//
+// Same positional scene names and flags as the clap `Cli` (src/main.rs:51-103),
+// same background table (:155-164), same image height rule
+// (H = (W as f32 / aspect) as usize, src/renderer.rs:34-39) and the same ASCII
+// P3 PPM on stdout (src/renderer.rs:107-127). The render itself runs on the
+// GPU through the C ABI; there is no CPU fallback.
+//
+// Extra flags (not in the reference): --seed N (the reference's thread_rng is
+// OS-seeded), --assets DIR, --device N, --pfm FILE (linear float dump),
+// --exact-bvh.
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <chrono>
+#include <string>
+#include <vector>
+
+#include "../../include/rt.h"
+
+namespace {
+
+void usage() {
+    fprintf(stderr,
+            "Usage: shimmer <SCENE> [OPTIONS]\n"
+            "  SCENE: random-spheres random-moving-spheres two-spheres marble earth simple-lights\n"
+            "         cornell cornell-smoke showcase bunny gargoyle igea-hrpp\n"
+            "  -w, --image-width <W>            [default: 1080]\n"
+            "  -a, --aspect-ratio <X> <Y>       [default: 16 9]\n"
+            "  -s, --samples-per-pixel <N>      [default: 500]\n"
+            "  -d, --depth <N>                  [default: 50]\n"
+            "      --tile-width <N>             [default: 8]\n"
+            "      --tile-height <N>            [default: 8]\n"
+            "      --cam-look-from <X> <Y> <Z>  [default: 13 2 3]\n"
+            "      --cam-look-at <X> <Y> <Z>    [default: 0 0 0]\n"
+            "      --cam-view-up <X> <Y> <Z>    [default: 0 1 0]\n"
+            "      --cam-vertical-fov <DEG>     [default: 20]\n"
+            "      --cam-aperture <A>           [default: 0]\n"
+            "      --cam-focus-dist <D>         [default: 10]\n"
+            "      --cam-start-time <T>         [default: 0]\n"
+            "      --cam-end-time <T>           [default: 0]\n"
+            "      --seed <N> --assets <DIR> --device <N> --pfm <FILE> --exact-bvh\n");
+}
+
+bool parse_f(const char* s, float* out) {
+    char* end = nullptr;
+    *out = strtof(s, &end);
+    return end && *end == '\0';
+}
+bool parse_u(const char* s, unsigned long long* out) {
+    char* end = nullptr;
+    *out = strtoull(s, &end, 10);
+    return end && *end == '\0';
+}
+
+// palette 0.6.1 Srgb<f32> -> Srgb<u8> (restated: clamp to [0,1], scale, round).
+unsigned to_u8(float c) {
+    if (!(c > 0.0f)) c = 0.0f;
+    if (c > 1.0f) c = 1.0f;
+    return (unsigned)lroundf(c * 255.0f);
+}
+
+std::string default_assets(const char* argv0) {
+    std::string p(argv0);
+    size_t k = p.rfind('/');
+    std::string dir = k == std::string::npos ? "." : p.substr(0, k);
+    return dir + "/../../assets";
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    if (argc < 2) {
+        usage();
+        return 2;
+    }
+    std::string scene;
+    unsigned long long width = 1080, spp = 500, depth = 50, tw = 8, th = 8, seed = 1, device = 0;
+    float aspect[2] = {16.0f, 9.0f};
+    float from[3] = {13.0f, 2.0f, 3.0f}, at[3] = {0.0f, 0.0f, 0.0f}, up[3] = {0.0f, 1.0f, 0.0f};
+    float vfov = 20.0f, aperture = 0.0f, focus = 10.0f, t0 = 0.0f, t1 = 0.0f;
+    std::string assets = default_assets(argv[0]), pfm;
+    bool exact = false;
+    for (int i = 1; i < argc; ++i) {
+        std::string a = argv[i];
+        auto need = [&](int n) {
+            if (i + n >= argc) {
+                fprintf(stderr, "error: %s needs %d value(s)\n", a.c_str(), n);
+                exit(2);
+            }
+        };
+        auto fl = [&](float* dst, int n) {
+            need(n);
+            for (int k = 0; k < n; ++k)
+                if (!parse_f(argv[++i], &dst[k])) {
+                    fprintf(stderr, "error: bad number for %s\n", a.c_str());
+                    exit(2);
+                }
+        };
+        auto ul = [&](unsigned long long* dst) {
+            need(1);
+            if (!parse_u(argv[++i], dst)) {
+                fprintf(stderr, "error: bad integer for %s\n", a.c_str());
+                exit(2);
+            }
+        };
+        if (a == "-h" || a == "--help") { usage(); return 0; }
+        else if (a == "-w" || a == "--image-width") ul(&width);
+        else if (a == "-a" || a == "--aspect-ratio") fl(aspect, 2);
+        else if (a == "-s" || a == "--samples-per-pixel") ul(&spp);
+        else if (a == "-d" || a == "--depth") ul(&depth);
+        else if (a == "--tile-width") ul(&tw);
+        else if (a == "--tile-height") ul(&th);
+        else if (a == "--cam-look-from") fl(from, 3);
+        else if (a == "--cam-look-at") fl(at, 3);
+        else if (a == "--cam-view-up") fl(up, 3);
+        else if (a == "--cam-vertical-fov") fl(&vfov, 1);
+        else if (a == "--cam-aperture") fl(&aperture, 1);
+        else if (a == "--cam-focus-dist") fl(&focus, 1);
+        else if (a == "--cam-start-time") fl(&t0, 1);
+        else if (a == "--cam-end-time") fl(&t1, 1);
+        else if (a == "--seed") ul(&seed);
+        else if (a == "--device") ul(&device);
+        else if (a == "--assets") { need(1); assets = argv[++i]; }
+        else if (a == "--pfm") { need(1); pfm = argv[++i]; }
+        else if (a == "--exact-bvh") exact = true;
+        else if (!a.empty() && a[0] == '-') { fprintf(stderr, "error: unexpected argument '%s'\n", a.c_str()); usage(); return 2; }
+        else if (scene.empty()) scene = a;
+        else { fprintf(stderr, "error: unexpected argument '%s'\n", a.c_str()); return 2; }
+    }
+    if (scene.empty()) { usage(); return 2; }
+    float aspect_ratio = aspect[0] / aspect[1];                                   // main.rs:109
+    unsigned long long height = (unsigned long long)((float)width / aspect_ratio);  // renderer.rs:37
+
+    rt_camera_desc cam;
+    memset(&cam, 0, sizeof cam);
+    memcpy(cam.look_from, from, sizeof from);
+    memcpy(cam.look_at, at, sizeof at);
+    memcpy(cam.view_up, up, sizeof up);
+    cam.vfov_deg = vfov;
+    cam.aspect_ratio = aspect_ratio;
+    cam.aperture = aperture;
+    cam.focus_dist = focus;
+    cam.time0 = t0;
+    cam.time1 = t1;
+
+    auto start = std::chrono::steady_clock::now();  // main.rs:138
+    rt_scene_desc* desc = nullptr;
+    if (rt_scene_generate(scene.c_str(), seed, assets.c_str(), &desc) != RT_OK) {
+        fprintf(stderr, "error: %s\n", rt_last_error());
+        return 1;
+    }
+    rt_render_params p;
+    memset(&p, 0, sizeof p);
+    p.width = (uint32_t)width;
+    p.height = (uint32_t)height;
+    p.samples_per_pixel = (uint32_t)spp;
+    p.max_depth = (uint32_t)depth;
+    p.tile_width = (uint32_t)tw;
+    p.tile_height = (uint32_t)th;
+    p.seed = seed;
+    p.flags = exact ? RT_FLAG_EXACT_BVH : 0u;
+    if (rt_scene_background(scene.c_str(), p.background) != RT_OK) {
+        fprintf(stderr, "error: %s\n", rt_last_error());
+        return 1;
+    }
+    rt_scene_handle h = nullptr;
+    if (rt_scene_upload(desc, (int)device, &h) != RT_OK) {
+        fprintf(stderr, "error: %s\n", rt_last_error());
+        rt_scene_desc_free(desc);
+        return 1;
+    }
+    std::vector<float> img((size_t)width * height * 3u, 0.0f);
+    rt_stats st;
+    fprintf(stderr, "Rendering tiles...\n");
+    if (rt_render(h, &cam, &p, img.data(), &st) != RT_OK) {
+        fprintf(stderr, "error: %s\n", rt_last_error());
+        rt_scene_free(h);
+        rt_scene_desc_free(desc);
+        return 1;
+    }
+    fprintf(stderr, "\nDone tracing.\nWriting to file...\n");
+    std::string outbuf;
+    outbuf.reserve((size_t)width * height * 12u + 32u);
+    char line[64];
+    snprintf(line, sizeof line, "P3\n%llu %llu\n255\n", width, height);
+    outbuf += line;
+    for (long long y = (long long)height - 1; y >= 0; --y)
+        for (unsigned long long x = 0; x < width; ++x) {
+            const float* c = &img[((size_t)y * width + x) * 3u];
+            snprintf(line, sizeof line, "%u %u %u\n", to_u8(c[0]), to_u8(c[1]), to_u8(c[2]));
+            outbuf += line;
+        }
+    fwrite(outbuf.data(), 1, outbuf.size(), stdout);
+    fflush(stdout);
+    fprintf(stderr, "Done writing to file.\n");
+    if (!pfm.empty()) {
+        FILE* f = fopen(pfm.c_str(), "wb");
+        if (f) {
+            fprintf(f, "PF\n%llu %llu\n-1.0\n", width, height);  // PFM rows are bottom-up, like ours
+            fwrite(img.data(), sizeof(float), img.size(), f);
+            fclose(f);
+        }
+    }
+    rt_scene_free(h);
+    rt_scene_desc_free(desc);
+    double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - start).count();
+    fprintf(stderr, "Render time: %.3fs (kernel %.3f ms, %llu samples, %llu segments)\n", secs, st.kernel_ms,
+            (unsigned long long)st.samples, (unsigned long long)st.segments);
+    return 0;
+}

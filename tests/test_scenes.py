@@ -1,0 +1,85 @@
+"""Scene generators (src/main.rs:185-829 restated): structure and determinism."""
+import numpy as np
+import pytest
+
+from raytracinginoneweekendinrust_amd import _capi as K
+
+ALL = ["random-spheres", "random-spheres-nobvh", "random-moving-spheres", "two-spheres", "marble", "earth",
+       "simple-lights", "cornell", "cornell-smoke", "showcase", "bunny"]
+
+
+@pytest.mark.parametrize("name", ALL)
+def test_generation_is_deterministic(name, rt):
+    a = rt.Scene.generate(name, 7).nodes()
+    b = rt.Scene.generate(name, 7).nodes()
+    assert a.tobytes() == b.tobytes()
+
+
+def test_seed_changes_random_scenes(rt):
+    a = rt.Scene.generate("random-spheres", 1).nodes()
+    b = rt.Scene.generate("random-spheres", 2).nodes()
+    assert a.tobytes() != b.tobytes()
+
+
+def count(nodes, kind):
+    return int((nodes["kind"] == kind).sum())
+
+
+def test_random_spheres_structure(rt):
+    n = rt.Scene.generate("random-spheres", 20231).nodes()
+    spheres = count(n, K.RT_OBJ_SPHERE)
+    assert 4 + 400 <= spheres <= 4 + 484  # ground + <=484 small + 3 big (main.rs:199-244)
+    assert count(n, K.RT_OBJ_BVH) == 1
+    small = n[(n["kind"] == K.RT_OBJ_SPHERE) & np.isclose(n["f"][:, 3], 0.2)]
+    assert np.all(small["f"][:, 1] == np.float32(0.2))
+    metals = n[n["kind"] == K.RT_MAT_METAL]
+    assert np.all(metals["f"][:, 3] <= 0.5)
+
+
+def test_showcase_structure(rt):
+    n = rt.Scene.generate("showcase", 20231).nodes()
+    cubes = n[n["kind"] == K.RT_OBJ_CUBE]
+    assert len(cubes) == 400
+    y1 = cubes["f"][:, 4]
+    assert np.all((y1 >= 1.0) & (y1 < 101.0))
+    assert count(n, K.RT_OBJ_BVH) == 2
+    assert count(n, K.RT_OBJ_CONSTANT_MEDIUM) == 2
+    assert count(n, K.RT_OBJ_MOVING_SPHERE) == 1
+    assert count(n, K.RT_TEX_IMAGE) == 1 and count(n, K.RT_TEX_MARBLE) == 1
+    small = n[(n["kind"] == K.RT_OBJ_SPHERE) & (n["f"][:, 3] == 10.0)]
+    assert len(small) == 1000
+    assert np.all((small["f"][:, :3] >= 0) & (small["f"][:, :3] < 165))
+
+
+def test_bunny_substitute_mesh(rt):
+    n = rt.Scene.generate("bunny", 20231).nodes()
+    tris = n[n["kind"] == K.RT_OBJ_TRI]
+    assert len(tris) == 20480
+    ys = tris["f"][:, [1, 4, 7]]
+    assert ys.min() >= 0.0 and ys.max() < 300
+
+
+def test_nobvh_variant_has_the_same_spheres(rt):
+    a = rt.Scene.generate("random-spheres", 5).nodes()
+    b = rt.Scene.generate("random-spheres-nobvh", 5).nodes()
+    sa = a[a["kind"] == K.RT_OBJ_SPHERE]
+    sb = b[b["kind"] == K.RT_OBJ_SPHERE]
+    assert sa.tobytes() == sb.tobytes()
+
+
+@pytest.mark.parametrize("name", ["gargoyle", "igea-hrpp"])
+def test_lfs_mesh_scenes_need_assets(name, rt):
+    with pytest.raises(rt.RTError) as e:
+        rt.Scene.generate(name, 1)
+    assert e.value.code == -6
+
+
+def test_obj_loader_fan_triangulates(rt, tmp_path):
+    (tmp_path / "bunny_2000_scale.obj").write_text(
+        "v 0 0 0\nv 1 0 0\nv 1 1 0\nv 0 1 0\nf 1 2 3 4\nf -4/1/1 -3/2/2 -2/3/3\n")
+    (tmp_path / "earthmap_1024x512.rgb8").write_bytes(b"")
+    n = rt.Scene.generate("bunny", 1, str(tmp_path)).nodes()
+    tris = n[n["kind"] == K.RT_OBJ_TRI]
+    assert len(tris) == 3
+    np.testing.assert_array_equal(tris["f"][0][:9], [0, 0, 0, 1, 0, 0, 1, 1, 0])
+    np.testing.assert_array_equal(tris["f"][1][:9], [0, 0, 0, 1, 1, 0, 0, 1, 0])
