@@ -20,6 +20,7 @@
 // has no dense contraction.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <string>
@@ -110,11 +111,15 @@ RT_DEV void philox(uint32_t& c0, uint32_t& c1, uint32_t& c2, uint32_t& c3, uint3
 struct Key {
     uint32_t k0, k1;
 };
+__device__ __noinline__ uint4 philox_block(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t k0, uint32_t k1) {
+    uint32_t c3 = 0u;
+    philox(c0, c1, c2, c3, k0, k1);
+    return make_uint4(c0, c1, c2, c3);
+}
 RT_DEV uint32_t next_u32(Rng& g, const Key& k) {
     if (g.n == 0u) {
-        uint32_t c0 = g.block, c1 = g.sample, c2 = g.pixel, c3 = 0u;
-        philox(c0, c1, c2, c3, k.k0, k.k1);
-        g.b0 = c0; g.b1 = c1; g.b2 = c2; g.b3 = c3;
+        uint4 b = philox_block(g.block, g.sample, g.pixel, k.k0, k.k1);
+        g.b0 = b.x; g.b1 = b.y; g.b2 = b.z; g.b3 = b.w;
         g.block += 1u;
         g.n = 4u;
     }
@@ -168,7 +173,37 @@ RT_DEV RayD to_d(const Ray& r) {
     return q;
 }
 
-// sphere.rs:49-103 — quadratic in f64
+// sphere.rs:57-82 — quadratic in f64; both candidate roots (the reference computes
+// the far root only when the near one is rejected: same IEEE values either way).
+struct Roots {
+    double r1, r2;
+    bool ok;
+};
+RT_DEV Roots sphere_roots(f4 s, const RayD& q) {
+    double ocx = q.ox - (double)s.x, ocy = q.oy - (double)s.y, ocz = q.oz - (double)s.z;
+    double rad = (double)s.w;
+    double half_b = (ocx * q.dx + ocy * q.dy) + ocz * q.dz;
+    double c = ((ocx * ocx + ocy * ocy) + ocz * ocz) - rad * rad;
+    double disc = half_b * half_b - q.a * c;
+    Roots R;
+    R.ok = !sign_negative_d(disc);
+    double sq = __builtin_sqrt(disc);
+    R.r1 = (-half_b - sq) / q.a;
+    R.r2 = (-half_b + sq) / q.a;
+    return R;
+}
+// sphere.rs:83-89 — near root unless outside [t_min, t_max], then the far root.
+RT_DEV bool sphere_select(const Roots& R, float tmin, float tmax, float& t) {
+    if (!R.ok) return false;
+    double root = R.r1;
+    if (root < (double)tmin || (double)tmax < root) {
+        root = R.r2;
+        if (root < (double)tmin || (double)tmax < root) return false;
+    }
+    t = (float)root;
+    return true;
+}
+// sphere.rs:49-103
 RT_DEV bool sphere_t(f4 s, const RayD& q, float tmin, float tmax, float& t) {
     double ocx = q.ox - (double)s.x, ocy = q.oy - (double)s.y, ocz = q.oz - (double)s.z;
     double rad = (double)s.w;
@@ -397,9 +432,20 @@ RT_DEV bool medium_hit(const DevScene& S, const DevEntry* E, Ray r, float tmin, 
     for (uint32_t i = 0; i < ntf; ++i) r = apply_op(E->tf[i], r);
     const DevEntry* B = S.entries + E->payload;
     float t1 = kInf, t2 = kInf;
-    uint32_t dummy;
-    if (!entry_geom_hit(S, B, r, -kInf, t1, dummy, stk, exact)) return false;
-    if (!entry_geom_hit(S, B, r, t1 + 0.0001f, t2, dummy, stk, exact)) return false;
+    if (B->kind == rtdev::kEntGeom && rtdev::leaf_type(B->payload) == rtdev::kLeafSphere) {
+        // boundary.hit(-inf, inf) then boundary.hit(t1 + 1e-4, inf) on one sphere:
+        // the same two roots, selected against two intervals.
+        Ray rb = r;
+        uint32_t bn = B->ntf;
+        for (uint32_t i = 0; i < bn; ++i) rb = apply_op(B->tf[i], rb);
+        Roots R = sphere_roots(ld4(S.sph + rtdev::leaf_index(B->payload)), to_d(rb));
+        if (!sphere_select(R, -kInf, kInf, t1)) return false;
+        if (!sphere_select(R, t1 + 0.0001f, kInf, t2)) return false;
+    } else {
+        uint32_t dummy;
+        if (!entry_geom_hit(S, B, r, -kInf, t1, dummy, stk, exact)) return false;
+        if (!entry_geom_hit(S, B, r, t1 + 0.0001f, t2, dummy, stk, exact)) return false;
+    }
     if (t1 < tmin) t1 = tmin;
     if (t2 > tmax) t2 = tmax;
     if (t1 >= t2) return false;
@@ -594,7 +640,7 @@ RT_DEV double fbm_get(const uint8_t* tabs, uint32_t seed0, double x, double y, d
     }
     return result * scale_factor;
 }
-RT_DEV double turbulence(const uint8_t* tabs, double px, double py, double pz) {
+__device__ __noinline__ double turbulence(const uint8_t* tabs, double px, double py, double pz) {
     const double power = 1.0;
     double xd = px + fbm_get(tabs, 0u, px + 12414.0 / 65536.0, py + 65124.0 / 65536.0, pz + 31337.0 / 65536.0) * power;
     double yd = py + fbm_get(tabs, 1u, px + 26519.0 / 65536.0, py + 18128.0 / 65536.0, pz + 60493.0 / 65536.0) * power;
@@ -649,8 +695,13 @@ RT_DEV bool scatter(const DevScene& S, const DevMaterial& m, const Ray& r, const
                     V& att, Ray& sc) {
     sc.o = rec.p;
     sc.time = r.time;
+    // Lambertian, Metal and Isotropic each draw exactly one in_unit_sphere() and
+    // nothing else (lambertian.rs:36, metal.rs:30, isotropic.rs:37): draw it once here.
+    V rs = mk(0.0f, 0.0f, 0.0f);
+    if (m.kind == rtdev::kMatLambertian || m.kind == rtdev::kMatMetal || m.kind == rtdev::kMatIsotropic)
+        rs = in_unit_sphere(g, k);
     if (m.kind == rtdev::kMatLambertian) {  // lambertian.rs:34-53
-        V dir = rec.n + normalize(in_unit_sphere(g, k));
+        V dir = rec.n + normalize(rs);
         if (near_zero(dir)) dir = rec.n;
         sc.d = dir;
         att = tex_value(S, m.tex, rec.u, rec.v, rec.p);
@@ -658,7 +709,7 @@ RT_DEV bool scatter(const DevScene& S, const DevMaterial& m, const Ray& r, const
     }
     if (m.kind == rtdev::kMatMetal) {  // metal.rs:25-43
         V reflected = reflect(normalize(r.d), rec.n);
-        V dir = reflected + m.fuzz * in_unit_sphere(g, k);
+        V dir = reflected + m.fuzz * rs;
         sc.d = dir;
         att = mk(m.albedo[0], m.albedo[1], m.albedo[2]);
         return dot(dir, rec.n) > 0.0f;
@@ -683,7 +734,7 @@ RT_DEV bool scatter(const DevScene& S, const DevMaterial& m, const Ray& r, const
         return true;
     }
     if (m.kind == rtdev::kMatIsotropic) {  // isotropic.rs:31-43
-        sc.d = in_unit_sphere(g, k);
+        sc.d = rs;
         att = tex_value(S, m.tex, rec.u, rec.v, rec.p);
         return true;
     }
@@ -694,8 +745,8 @@ RT_DEV bool scatter(const DevScene& S, const DevMaterial& m, const Ray& r, const
 // the kernel
 // ---------------------------------------------------------------------------
 RT_DEV void start_sample(const DevCamera& C, const DevParams& P, const Key& k, uint32_t x, uint32_t y,
-                         uint32_t pixel, uint32_t s, Rng& g, Ray& ray) {
-    g.sample = P.sample_base + s;
+                         uint32_t pixel, uint32_t sample, Rng& g, Ray& ray) {
+    g.sample = sample;
     g.pixel = pixel;
     g.block = 0u;
     g.n = 0u;
@@ -716,28 +767,94 @@ RT_DEV void start_sample(const DevCamera& C, const DevParams& P, const Key& k, u
     ray.time = v01 * C.time_scale + C.time_low;
 }
 
-__global__ __launch_bounds__(64) void render_blocks(DevScene S, DevCamera C, DevParams P, float* __restrict__ out,
+// One launch covers samples [sample0, sample0 + samples) of every pixel of the shard.
+// Work items are (8x8 block, sample, pixel-in-block); a "batch" is kGroup
+// consecutive samples of one block (64 * kGroup items), blocks in shard order.
+constexpr uint32_t kGroup = 8;
+struct ChunkParams {
+    uint32_t sample0;         // global sample index of chunk sample 0 (includes P.sample_base)
+    uint32_t samples;         // samples per pixel in this chunk
+    uint32_t groups_per_block;
+    uint32_t num_batches;
+    uint32_t npix;            // width * height (sample-buffer plane size)
+};
+
+// Renderer::get_color's sample loop (renderer.rs:140-146) as a work pool. Each
+// lane owns one camera sample at a time; when its path ends (ray.rs:32-62) it
+// stores the sample's radiance in the HBM sample buffer and takes the next item.
+// Idle lanes are refilled with a wave ballot + mbcnt from a wave-local batch, and
+// a batch costs one atomic, so no lane waits for a neighbour's long path.
+// resolve_samples() then sums every pixel's samples IN SAMPLE ORDER, exactly like
+// `color_accumulator +=` in the reference.
+__global__ __launch_bounds__(64) void trace_samples(DevScene S, DevCamera C, DevParams P, ChunkParams Q,
+                                                     float* __restrict__ sbuf, unsigned* __restrict__ batch_counter,
                                                      unsigned long long* __restrict__ seg_counter) {
     extern __shared__ uint32_t lds_stack[];
     const uint32_t lane = threadIdx.x;
     uint32_t* stk = lds_stack + lane;
-    const uint32_t blk = P.shard_index + blockIdx.x * P.shard_count;
-    const uint32_t bx = blk % P.blocks_x, by = blk / P.blocks_x;
-    const uint32_t x = bx * 8u + (lane & 7u), y = by * 8u + (lane >> 3);
-    const bool valid = blk < P.num_blocks && x < P.width && y < P.height;
     const Key k{P.seed_lo, P.seed_hi};
     const bool exact = (P.flags & RT_FLAG_EXACT_BVH) != 0u;
     const V bg = mk(P.bg[0], P.bg[1], P.bg[2]);
-    uint32_t nseg = 0;
-    if (valid) {
-        const uint32_t pixel = y * P.width + x;
-        V acc = mk(0.0f, 0.0f, 0.0f);
-        V L = mk(0.0f, 0.0f, 0.0f), T = mk(1.0f, 1.0f, 1.0f);
-        Rng g;
-        Ray ray;
-        uint32_t s = 0, depth = P.max_depth;
-        start_sample(C, P, k, x, y, pixel, s, g, ray);
+
+    bool has = false;
+    uint32_t pixel = 0, s_local = 0, depth = 0, nseg = 0;
+    V L = mk(0.0f, 0.0f, 0.0f), T = mk(1.0f, 1.0f, 1.0f);
+    Rng g;
+    g.sample = g.pixel = g.block = g.n = 0u;
+    g.b0 = g.b1 = g.b2 = g.b3 = 0u;
+    Ray ray;
+    ray.o = ray.d = mk(0.0f, 0.0f, 0.0f);
+    ray.time = 0.0f;
+    uint32_t pool_batch = 0, pool_next = 0, pool_end = 0;  // wave-uniform
+    bool exhausted = false;                                 // wave-uniform
+
+    for (;;) {
+        // ---- hand items to idle lanes ------------------------------------
         for (;;) {
+            unsigned long long need = __ballot(!has);
+            if (need == 0ull || exhausted) break;
+            if (pool_next == pool_end) {
+                uint32_t bt = 0;
+                if (lane == 0u) bt = atomicAdd(batch_counter, 1u);
+                bt = __builtin_amdgcn_readfirstlane(bt);
+                if (bt >= Q.num_batches) {
+                    exhausted = true;
+                    break;
+                }
+                pool_batch = bt;
+                pool_next = 0u;
+                pool_end = 64u * kGroup;
+                continue;
+            }
+            uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
+                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
+            uint32_t avail = pool_end - pool_next;
+            if (!has && rank < avail) {
+                uint32_t item = pool_next + rank;
+                uint32_t blk_local = pool_batch / Q.groups_per_block;
+                uint32_t grp = pool_batch - blk_local * Q.groups_per_block;
+                uint32_t s = grp * kGroup + (item >> 6);
+                uint32_t pib = item & 63u;
+                uint32_t blk = P.shard_index + blk_local * P.shard_count;
+                uint32_t by = blk / P.blocks_x, bx = blk - by * P.blocks_x;
+                uint32_t x = bx * 8u + (pib & 7u), y = by * 8u + (pib >> 3);
+                if (x < P.width && y < P.height && s < Q.samples) {
+                    has = true;
+                    pixel = y * P.width + x;
+                    s_local = s;
+                    L = mk(0.0f, 0.0f, 0.0f);
+                    T = mk(1.0f, 1.0f, 1.0f);
+                    depth = P.max_depth;
+                    start_sample(C, P, k, x, y, pixel, Q.sample0 + s, g, ray);
+                }
+            }
+            uint32_t n = (uint32_t)__popcll(need);
+            pool_next += n < avail ? n : avail;
+        }
+        if (__ballot(has) == 0ull) break;  // pool exhausted and every path finished
+
+        // ---- one ray segment per live lane (ray.rs:32-62) -----------------
+        if (has) {
             bool done;
             if (depth == 0u) {
                 done = true;  // ray.rs:39-41
@@ -767,26 +884,42 @@ __global__ __launch_bounds__(64) void render_blocks(DevScene S, DevCamera C, Dev
                 }
             }
             if (done) {
-                acc = acc + L;
-                s += 1u;
-                if (s >= P.spp) break;
-                L = mk(0.0f, 0.0f, 0.0f);
-                T = mk(1.0f, 1.0f, 1.0f);
-                depth = P.max_depth;
-                start_sample(C, P, k, x, y, pixel, s, g, ray);
+                float* o = sbuf + ((size_t)s_local * Q.npix + pixel) * 3u;
+                o[0] = L.x;
+                o[1] = L.y;
+                o[2] = L.z;
+                has = false;
             }
         }
-        V col = divs(acc, (float)P.spp);  // renderer.rs:147
-        float* o = out + (size_t)pixel * 3u;
-        o[0] = col.x;
-        o[1] = col.y;
-        o[2] = col.z;
     }
     if (seg_counter) {
         unsigned long long v = nseg;
         for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
         if (lane == 0u) atomicAdd(seg_counter, v);
     }
+}
+
+// color_accumulator += ray_color(...) in sample order, then / spp (renderer.rs:140-147).
+// Chunks continue the same running sum held in `out`.
+__global__ __launch_bounds__(256) void resolve_samples(const float* __restrict__ sbuf, float* __restrict__ out,
+                                                        DevParams P, ChunkParams Q, int first, int last) {
+    uint32_t p = blockIdx.x * 256u + threadIdx.x;
+    if (p >= Q.npix) return;
+    uint32_t y = p / P.width, x = p - y * P.width;
+    uint32_t blk = (y >> 3) * P.blocks_x + (x >> 3);
+    if (P.shard_count > 1u && blk % P.shard_count != P.shard_index) return;
+    float* o = out + (size_t)p * 3u;
+    V acc = first ? mk(0.0f, 0.0f, 0.0f) : mk(o[0], o[1], o[2]);
+    const float* src = sbuf + (size_t)p * 3u;
+    const size_t plane = (size_t)Q.npix * 3u;
+    for (uint32_t s = 0; s < Q.samples; ++s) {
+        acc = acc + mk(src[0], src[1], src[2]);
+        src += plane;
+    }
+    if (last) acc = divs(acc, (float)P.spp);
+    o[0] = acc.x;
+    o[1] = acc.y;
+    o[2] = acc.z;
 }
 
 // Device numeric self-check (rt_device_numeric_eval).
@@ -820,6 +953,12 @@ struct rt_scene {
     uint64_t pool_bytes = 0;
     DevScene dev{};
     uint64_t counts[10] = {};
+    // render workspace (sample buffer + batch counter), grown on demand; one render
+    // at a time per scene handle
+    float* sbuf = nullptr;
+    uint64_t sbuf_bytes = 0;
+    unsigned* counter = nullptr;
+    int grid = 0;  // resident waves of trace_samples
 };
 
 namespace {
@@ -962,6 +1101,8 @@ int rt_scene_free(rt_scene_handle s) {
     {
         DeviceGuard g(s->device);
         if (s->pool) (void)hipFree(s->pool);
+        if (s->sbuf) (void)hipFree(s->sbuf);
+        if (s->counter) (void)hipFree(s->counter);
     }
     delete s;
     return RT_OK;
@@ -1002,13 +1143,58 @@ int rt_render_launch(rt_scene_handle s, const rt_camera_desc* camera, const rt_r
     dp.bg[2] = p->background[2];
     uint32_t nblk = dp.num_blocks > dp.shard_index ? (dp.num_blocks - dp.shard_index + dp.shard_count - 1u) / dp.shard_count : 0u;
     if (nblk == 0) return RT_OK;
-    size_t lds = (size_t)s->dev.stack_depth * 64u * sizeof(uint32_t);
     DeviceGuard g(s->device);
     if (!g.ok) return rthost::set_error(RT_ERR_HIP, "hipSetDevice failed");
-    hipLaunchKernelGGL(render_blocks, dim3(nblk), dim3(64), lds, (hipStream_t)stream, s->dev, cam, dp, d_out,
-                       d_segments);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return hip_fail(e, "render_blocks launch");
+    // Sample buffer: chunks of whole sample ranges (the per-pixel sum stays in order).
+    const uint64_t npix = (uint64_t)p->width * p->height;
+    const uint64_t per_sample = npix * 3u * sizeof(float);
+    uint64_t budget = 4096ull << 20;
+    if (const char* env = getenv("RT_SAMPLE_BUFFER_MB")) budget = strtoull(env, nullptr, 10) << 20;
+    uint64_t max_s = budget / per_sample;
+    if (max_s < 1) max_s = 1;
+    uint32_t nchunks = (uint32_t)((p->samples_per_pixel + max_s - 1) / max_s);
+    uint32_t chunk = (p->samples_per_pixel + nchunks - 1) / nchunks;
+    uint64_t need = per_sample * chunk;
+    hipError_t e;
+    if (s->sbuf_bytes < need) {
+        if (s->sbuf) (void)hipFree(s->sbuf);
+        s->sbuf = nullptr;
+        s->sbuf_bytes = 0;
+        if ((e = hipMalloc(&s->sbuf, need)) != hipSuccess)
+            return rthost::set_error(RT_ERR_OOM, std::string("hipMalloc sample buffer: ") + hipGetErrorString(e));
+        s->sbuf_bytes = need;
+    }
+    if (!s->counter) {
+        if ((e = hipMalloc(&s->counter, 256)) != hipSuccess)
+            return rthost::set_error(RT_ERR_OOM, std::string("hipMalloc counter: ") + hipGetErrorString(e));
+    }
+    size_t lds = (size_t)s->dev.stack_depth * 64u * sizeof(uint32_t);
+    if (s->grid == 0) {
+        int per_cu = 0, cus = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace_samples, 64, lds) != hipSuccess || per_cu < 1)
+            per_cu = 8;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s->device) != hipSuccess || cus < 1)
+            cus = 256;
+        s->grid = per_cu * cus;
+    }
+    hipStream_t st = (hipStream_t)stream;
+    for (uint32_t c = 0; c < nchunks; ++c) {
+        ChunkParams q;
+        q.sample0 = p->sample_base + c * chunk;
+        q.samples = c + 1 < nchunks ? chunk : p->samples_per_pixel - c * chunk;
+        q.groups_per_block = (q.samples + kGroup - 1) / kGroup;
+        q.num_batches = nblk * q.groups_per_block;
+        q.npix = (uint32_t)npix;
+        if ((e = hipMemsetAsync(s->counter, 0, sizeof(unsigned), st)) != hipSuccess) return hip_fail(e, "memset counter");
+        uint32_t grid = (uint32_t)s->grid;
+        if (grid > q.num_batches) grid = q.num_batches;
+        hipLaunchKernelGGL(trace_samples, dim3(grid), dim3(64), lds, st, s->dev, cam, dp, q, s->sbuf, s->counter,
+                           d_segments);
+        if ((e = hipGetLastError()) != hipSuccess) return hip_fail(e, "trace_samples launch");
+        hipLaunchKernelGGL(resolve_samples, dim3((uint32_t)((npix + 255u) / 256u)), dim3(256), 0, st, s->sbuf, d_out, dp,
+                           q, c == 0 ? 1 : 0, c + 1 == nchunks ? 1 : 0);
+        if ((e = hipGetLastError()) != hipSuccess) return hip_fail(e, "resolve_samples launch");
+    }
     return RT_OK;
 }
 
