@@ -66,13 +66,14 @@ struct alignas(16) DevEntry {
 static_assert(sizeof(DevEntry) == 80, "DevEntry layout");
 
 enum MatKind : uint32_t { kMatLambertian = 0, kMatMetal = 1, kMatDielectric = 2, kMatLight = 3, kMatIsotropic = 4 };
+constexpr uint32_t kMatNeedsUV = 1u;  // some texture of the material reads (u, v): an ImageTexture
 struct alignas(16) DevMaterial {
     uint32_t kind;
     uint32_t tex;
     float fuzz;
     float ior;
     float albedo[3];
-    float pad;
+    uint32_t flags;
 };
 static_assert(sizeof(DevMaterial) == 32, "DevMaterial layout");
 

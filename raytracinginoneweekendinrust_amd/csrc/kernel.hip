@@ -203,7 +203,10 @@ RT_DEV bool sphere_select(const Roots& R, float tmin, float tmax, float& t) {
     t = (float)root;
     return true;
 }
-// sphere.rs:49-103
+// sphere.rs:49-103. Before dividing, spheres whose near root is certainly beyond
+// t_max, or whose far root is certainly before t_min, are rejected: with the
+// 2^-40 margin the rounded quotient provably lies on the same side, so the
+// reference would reject both roots too ("division-free rejects").
 RT_DEV bool sphere_t(f4 s, const RayD& q, float tmin, float tmax, float& t) {
     double ocx = q.ox - (double)s.x, ocy = q.oy - (double)s.y, ocz = q.oz - (double)s.z;
     double rad = (double)s.w;
@@ -212,9 +215,15 @@ RT_DEV bool sphere_t(f4 s, const RayD& q, float tmin, float tmax, float& t) {
     double disc = half_b * half_b - q.a * c;
     if (sign_negative_d(disc)) return false;
     double sq = __builtin_sqrt(disc);
-    double root = (-half_b - sq) / q.a;
+    double n1 = -half_b - sq, n2 = -half_b + sq;
+    if (q.a > 0.0 && q.a < 1.0e300) {
+        const double up = 1.0 + 0x1p-40, down = 1.0 - 0x1p-40;
+        if (tmax > 0.0f && tmax < kInf && n1 > ((double)tmax * q.a) * up) return false;
+        if (tmin > 0.0f && n2 < ((double)tmin * q.a) * down) return false;
+    }
+    double root = n1 / q.a;
     if (root < (double)tmin || (double)tmax < root) {
-        root = (-half_b + sq) / q.a;
+        root = n2 / q.a;
         if (root < (double)tmin || (double)tmax < root) return false;
     }
     t = (float)root;
@@ -495,7 +504,7 @@ struct Rec {
     bool front;
     uint32_t mat;
 };
-RT_DEV void sphere_uv(V p, float& u, float& v) {  // sphere.rs:41-46
+__device__ __noinline__ void sphere_uv(V p, float& u, float& v) {  // sphere.rs:41-46
     const float PI = 3.14159265358979323846f;
     const float TWO_PI = 2.0f * PI;
     float theta = rt_acosf(-p.y);
@@ -512,36 +521,42 @@ RT_DEV void rec_new(Rec& rec, const Ray& r, V outward, float t, float u, float v
     rec.v = v;
     rec.mat = mat;
 }
+// (u, v) are computed only when the material reads them (kMatNeedsUV): they have
+// no side effects, so skipping them elsewhere changes no bit of the output.
+RT_DEV bool needs_uv(const DevScene& S, uint32_t mat) { return (S.mats[mat].flags & rtdev::kMatNeedsUV) != 0u; }
 RT_DEV void prim_record(const DevScene& S, uint32_t code, const Ray& r, float t, Rec& rec) {
     uint32_t type = rtdev::leaf_type(code), idx = rtdev::leaf_index(code);
+    float u = 0.0f, v = 0.0f;
     if (type == rtdev::kLeafSphere) {
         f4 s = ld4(S.sph + idx);
+        uint32_t mat = S.sph_mat[idx];
         V p = at(r, t);
         V n = divs(p - xyz(s), s.w);
-        float u, v;
-        sphere_uv(n, u, v);
-        rec_new(rec, r, n, t, u, v, S.sph_mat[idx]);
+        if (needs_uv(S, mat)) sphere_uv(n, u, v);
+        rec_new(rec, r, n, t, u, v, mat);
     } else if (type == rtdev::kLeafRect) {
         f4 r0 = ld4(S.rect + 2 * idx), r1 = ld4(S.rect + 2 * idx + 1);
-        uint32_t axis = __float_as_uint(r1.y);
-        float ok, dk, oa, da, ob, db;
-        rect_axes(axis, r, ok, dk, oa, da, ob, db);
-        float x = oa + t * da, y = ob + t * db;
-        float u = (x - r0.y) / (r0.z - r0.y);
-        float v = (y - r0.w) / (r1.x - r0.w);
+        uint32_t axis = __float_as_uint(r1.y), mat = __float_as_uint(r1.z);
+        if (needs_uv(S, mat)) {
+            float ok, dk, oa, da, ob, db;
+            rect_axes(axis, r, ok, dk, oa, da, ob, db);
+            float x = oa + t * da, y = ob + t * db;
+            u = (x - r0.y) / (r0.z - r0.y);
+            v = (y - r0.w) / (r1.x - r0.w);
+        }
         V n = axis == 0u ? mk(0.0f, 0.0f, 1.0f) : (axis == 1u ? mk(0.0f, 1.0f, 0.0f) : mk(1.0f, 0.0f, 0.0f));
-        rec_new(rec, r, n, t, u, v, __float_as_uint(r1.z));
+        rec_new(rec, r, n, t, u, v, mat);
     } else if (type == rtdev::kLeafTri) {
         f4 t0 = ld4(S.tri + 3 * idx), t1 = ld4(S.tri + 3 * idx + 1), t2 = ld4(S.tri + 3 * idx + 2);
         V n = normalize(cross(xyz(t1), xyz(t2)));
         rec_new(rec, r, n, t, 0.0f, 0.0f, __float_as_uint(t0.w));
     } else {  // moving sphere
         f4 m0 = ld4(S.msph + 3 * idx), m1 = ld4(S.msph + 3 * idx + 1), m2 = ld4(S.msph + 3 * idx + 2);
+        uint32_t mat = __float_as_uint(m2.y);
         V p = at(r, t);
         V n = divs(p - msphere_center(m0, m1, m2, r.time), m0.w);
-        float u, v;
-        sphere_uv(n, u, v);
-        rec_new(rec, r, n, t, u, v, __float_as_uint(m2.y));
+        if (needs_uv(S, mat)) sphere_uv(n, u, v);
+        rec_new(rec, r, n, t, u, v, mat);
     }
 }
 RT_DEV void make_record(const DevScene& S, uint32_t entry, uint32_t code, float t, const Ray& r0, Rec& rec) {

@@ -340,11 +340,23 @@ class Lowerer {
                 return fail(RT_ERR_INVALID, "node " + std::to_string(idx) + " is not a material");
         }
         if (rc) return rc;
+        if ((m.kind == rtdev::kMatLambertian || m.kind == rtdev::kMatLight || m.kind == rtdev::kMatIsotropic) &&
+            texture_reads_uv(m.tex))
+            m.flags |= rtdev::kMatNeedsUV;
         uint32_t id = (uint32_t)s_->mats.size();
         s_->mats.push_back(m);
         mat_memo_[idx] = id;
         *out = id;
         return RT_OK;
+    }
+
+    // Only ImageTexture::value reads (u, v) (image_texture.rs:21-52); Checker passes them
+    // through to its children, Solid and Marble ignore them.
+    bool texture_reads_uv(uint32_t t, int depth = 0) const {
+        const rtdev::DevTexture& x = s_->texs[t];
+        if (x.kind == rtdev::kTexImage) return true;
+        if (x.kind == rtdev::kTexChecker && depth < 64) return texture_reads_uv(x.a, depth + 1) || texture_reads_uv(x.b, depth + 1);
+        return false;
     }
 
     uint32_t phase_material(uint32_t tex) {  // Isotropic::new(texture), hittable.rs:159
@@ -354,6 +366,7 @@ class Lowerer {
         memset(&m, 0, sizeof m);
         m.kind = rtdev::kMatIsotropic;
         m.tex = tex;
+        if (texture_reads_uv(tex)) m.flags |= rtdev::kMatNeedsUV;
         uint32_t id = (uint32_t)s_->mats.size();
         s_->mats.push_back(m);
         phase_memo_[tex] = id;
