@@ -6,7 +6,7 @@
 //              Translate/RotateY chains folded into each entry), followed by
 //              the boundaries of ConstantMedium entries;
 //   prims      SoA float4 records for spheres / moving spheres / rects / tris;
-//   nodes[]    every BVH (src/bvh.rs) as 32-byte nodes in DFS preorder;
+//   nodes[]    every BVH (src/bvh.rs) as 64-byte BVH2 nodes in DFS preorder;
 //   materials / textures / Perlin permutation tables / RGB8 texels.
 // Everything is read-only during a render and a few MB at most, so it stays
 // resident in each XCD's L2 after the first touch.
@@ -36,6 +36,7 @@ constexpr uint32_t kLeafTri = 4u;      // index into tri (3 f4 each)
 constexpr uint32_t kLeafMedium = 6u;   // hit identifier of a ConstantMedium scatter point
 constexpr uint32_t kChildEmpty = 0xffffffffu;  // second child of a 1-object node (bvh.rs:261-264)
 constexpr uint32_t kMaxIndex = 0x0fffffffu;
+constexpr uint32_t kBvhPrunable = 1u;  // wrapper-node flag: closest-hit box pruning is exact for this BVH
 
 RTDEV_HD uint32_t leaf_code(uint32_t type, uint32_t index) {
     return kLeafBit | (type << 28) | index;
@@ -93,7 +94,11 @@ static_assert(sizeof(DevTexture) == 32, "DevTexture layout");
 //   msph : (c0, r) (c1 - c0, t0) (t1 - t0, mat, 0, 0)     moving_sphere.rs:47-51
 //   rect : (k, a0, a1, b0) (b1, axis, mat, 0)  axis 0 = XY, 1 = XZ, 2 = YZ
 //   tri  : (v0, mat) (v1 - v0, 0) (v2 - v0, 0)           triangle.rs:44-45
-//   node : (min, left) (max, right)   left/right: node index or leaf code
+//   node : 64 B BVH2 node: (Lmin, Lmax.x) (Lmax.yz, Rmin.xy) (Rmin.z, Rmax)
+//          (left, right, left rank, right rank); left/right = node index or leaf
+//          code; a leaf child has no box (tested whenever its parent is visited).
+//          Each BVH starts with a wrapper node whose only child is the root; its
+//          left-rank field holds kBvhPrunable when every leaf is a Sphere/Rect/Cube.
 struct DevScene {
     const DevEntry* entries;
     const f4* sph;
@@ -124,6 +129,7 @@ struct DevParams {
     uint32_t shard_index, shard_count, blocks_x, num_blocks;
     uint32_t flags;
     float bg[3];
+    float prune_delta;  // box inflation for closest-hit pruning ("exact pruning")
 };
 
 }  // namespace rtdev

@@ -20,6 +20,7 @@
 // has no dense contraction.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <math.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -352,61 +353,155 @@ RT_DEV bool leaf_hit(const DevScene& S, uint32_t code, const Ray& r, const RayD&
 // aabb.rs:28-41 (Kensler). 1/d is hoisted per ray: the same IEEE quotient the
 // reference recomputes per node. All three slabs are evaluated branch-free; the
 // interval only shrinks, so this equals the reference's early-exit result.
-RT_DEV bool aabb_hit(f4 mn, f4 mx, const Ray& r, V inv, float t_min, float t_max) {
+// t_enter receives the final t_min (the ray's entry parameter into the box).
+RT_DEV bool slab(float x0, float y0, float z0, float x1, float y1, float z1, const Ray& r, V inv, float t_min,
+                 float t_max, float& t_enter) {
     {
-        float t0 = (mn.x - r.o.x) * inv.x, t1 = (mx.x - r.o.x) * inv.x;
+        float t0 = (x0 - r.o.x) * inv.x, t1 = (x1 - r.o.x) * inv.x;
         bool sw = inv.x < 0.0f;
         float a = sw ? t1 : t0, b = sw ? t0 : t1;
         t_min = a > t_min ? a : t_min;
         t_max = b < t_max ? b : t_max;
     }
     {
-        float t0 = (mn.y - r.o.y) * inv.y, t1 = (mx.y - r.o.y) * inv.y;
+        float t0 = (y0 - r.o.y) * inv.y, t1 = (y1 - r.o.y) * inv.y;
         bool sw = inv.y < 0.0f;
         float a = sw ? t1 : t0, b = sw ? t0 : t1;
         t_min = a > t_min ? a : t_min;
         t_max = b < t_max ? b : t_max;
     }
     {
-        float t0 = (mn.z - r.o.z) * inv.z, t1 = (mx.z - r.o.z) * inv.z;
+        float t0 = (z0 - r.o.z) * inv.z, t1 = (z1 - r.o.z) * inv.z;
         bool sw = inv.z < 0.0f;
         float a = sw ? t1 : t0, b = sw ? t0 : t1;
         t_min = a > t_min ? a : t_min;
         t_max = b < t_max ? b : t_max;
     }
+    t_enter = t_min;
     return !(t_max < t_min);
 }
 
-// BvhNode::hit (bvh.rs:363-417) as an iterative left-first DFS. Visiting order
-// and tie rule are the reference's; box tests prune with the running closest
-// hit unless `exact` (then they use the t_max the BVH was entered with, as the
-// reference does). The stack lives in LDS: stack[level * 64 + lane].
-RT_DEV bool bvh_hit(const DevScene& S, uint32_t root, const Ray& r, float tmin, float& closest, uint32_t& hit_code,
-                    uint32_t* stk, bool exact) {
+// A BVH leaf inside the traversal: candidates must beat (closest, best_rank)
+// lexicographically — smaller t, or equal t and later in the reference's DFS order.
+RT_DEV void leaf_hit_ranked(const DevScene& S, uint32_t code, uint32_t rank, const Ray& r, const RayD& q, float tmin,
+                            float& closest, uint32_t& best_rank, uint32_t& hit_code, bool& any) {
+    uint32_t type = rtdev::leaf_type(code), idx = rtdev::leaf_index(code);
+    float t;
+    if (type == rtdev::kLeafCube) {  // cube.rs:84-93: six sides, later faces win ties
+        for (uint32_t i = 0; i < 6u; ++i) {
+            uint32_t ri = idx + i;
+            if (rect_t(ld4(S.rect + 2 * ri), ld4(S.rect + 2 * ri + 1), r, tmin, closest, t) &&
+                (t < closest || rank + i > best_rank)) {
+                closest = t;
+                best_rank = rank + i;
+                hit_code = rtdev::leaf_code(rtdev::kLeafRect, ri);
+                any = true;
+            }
+        }
+        return;
+    }
+    bool h;
+    if (type == rtdev::kLeafSphere) h = sphere_t(ld4(S.sph + idx), q, tmin, closest, t);
+    else if (type == rtdev::kLeafTri) h = tri_t(ld4(S.tri + 3 * idx), ld4(S.tri + 3 * idx + 1), ld4(S.tri + 3 * idx + 2), r, tmin, closest, t);
+    else if (type == rtdev::kLeafRect) h = rect_t(ld4(S.rect + 2 * idx), ld4(S.rect + 2 * idx + 1), r, tmin, closest, t);
+    else h = msphere_t(ld4(S.msph + 3 * idx), ld4(S.msph + 3 * idx + 1), ld4(S.msph + 3 * idx + 2), r, tmin, closest, t);
+    if (h && (t < closest || rank > best_rank)) {
+        closest = t;
+        best_rank = rank;
+        hit_code = code;
+        any = true;
+    }
+}
+
+// Entry parameter of the ray into a box inflated by `delta` on every side (the
+// near-side half of the slab test above, on outward-rounded bounds).
+RT_DEV float slab_entry_inflated(float x0, float y0, float z0, float x1, float y1, float z1, const Ray& r, V inv,
+                                 float t_min, float delta) {
+    float ax = (inv.x < 0.0f ? (x1 + delta) - r.o.x : (x0 - delta) - r.o.x) * inv.x;
+    float ay = (inv.y < 0.0f ? (y1 + delta) - r.o.y : (y0 - delta) - r.o.y) * inv.y;
+    float az = (inv.z < 0.0f ? (z1 + delta) - r.o.z : (z0 - delta) - r.o.z) * inv.z;
+    t_min = ax > t_min ? ax : t_min;
+    t_min = ay > t_min ? ay : t_min;
+    t_min = az > t_min ? az : t_min;
+    return t_min;
+}
+// A subtree may be skipped once its inflated entry exceeds this bound: every
+// candidate inside it would then compute t > closest (exact pruning).
+RT_DEV float prune_bound(float closest) { return closest + __builtin_fabsf(closest) * 0x1p-19f; }
+
+// Bvh::hit / BvhNode::hit (bvh.rs:212-217, 363-417) as an iterative traversal of
+// BVH2 nodes. Every child box gets the reference's own test (stored box, the
+// t_max the BVH was entered with), so no node outside the reference's visit set
+// is ever entered. For BVHs flagged kBvhPrunable (f64 spheres / rects / cubes)
+// a visited subtree is additionally skipped when its entry into the box
+// inflated by P.prune_delta lies beyond prune_bound(closest): such a subtree
+// provably holds no candidate that could beat (closest, rank). Children are
+// visited nearest-first; ties resolve by DFS rank exactly like the recursion.
+// The stack lives in LDS, lane-strided: stack[level * 128 + {0, 64} + lane].
+RT_DEV bool bvh_hit(const DevScene& S, float delta, uint32_t root, const Ray& r, float tmin, float& closest,
+                    uint32_t& hit_code, uint32_t* stk, bool exact) {
     const float tmax_entry = closest;
+    const bool prune = !exact && (__float_as_uint(S.nodes[4 * (size_t)root + 3].z) & rtdev::kBvhPrunable) != 0u;
     V inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
     RayD q = to_d(r);
     bool any = false;
-    uint32_t sp = 0;
-    uint32_t cur = root;
+    uint32_t best_rank = 0, sp = 0, cur = root;
     for (;;) {
-        if (!(cur & rtdev::kLeafBit)) {
-            f4 a = ld4(S.nodes + 2 * cur), b = ld4(S.nodes + 2 * cur + 1);
-            if (aabb_hit(a, b, r, inv, tmin, exact ? tmax_entry : closest)) {
-                uint32_t right = __float_as_uint(b.w);
-                if (right != rtdev::kChildEmpty) {
-                    stk[sp * 64u] = right;
-                    sp += 1u;
-                }
-                cur = __float_as_uint(a.w);
-                continue;
-            }
+        const f4* nd = S.nodes + 4 * (size_t)cur;
+        f4 n0 = ld4(nd), n1 = ld4(nd + 1), n2 = ld4(nd + 2), n3 = ld4(nd + 3);
+        uint32_t lc = __float_as_uint(n3.x), rc = __float_as_uint(n3.y);
+        bool goL = false, goR = false;
+        float tl = 0.0f, tr = 0.0f;
+        if (lc & rtdev::kLeafBit) {
+            leaf_hit_ranked(S, lc, __float_as_uint(n3.z), r, q, tmin, closest, best_rank, hit_code, any);
         } else {
-            any |= leaf_hit(S, cur, r, q, tmin, closest, hit_code);
+            goL = slab(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, r, inv, tmin, tmax_entry, tl);
+            if (goL && prune) {
+                tl = slab_entry_inflated(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, r, inv, tmin, delta);
+                goL = !(tl > prune_bound(closest));
+            }
         }
-        if (sp == 0u) break;
-        sp -= 1u;
-        cur = stk[sp * 64u];
+        if (rc != rtdev::kChildEmpty) {
+            if (rc & rtdev::kLeafBit) {
+                leaf_hit_ranked(S, rc, __float_as_uint(n3.w), r, q, tmin, closest, best_rank, hit_code, any);
+            } else {
+                goR = slab(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, r, inv, tmin, tmax_entry, tr);
+                if (goR && prune) {
+                    tr = slab_entry_inflated(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, r, inv, tmin, delta);
+                    goR = !(tr > prune_bound(closest));
+                }
+            }
+        }
+        if (goL && goR) {
+            bool left_first = tl <= tr;
+            uint32_t far = left_first ? rc : lc;
+            float tfar = left_first ? tr : tl;
+            cur = left_first ? lc : rc;
+            stk[sp * 128u] = far;
+            stk[sp * 128u + 64u] = __float_as_uint(tfar);
+            sp += 1u;
+            continue;
+        }
+        if (goL) {
+            cur = lc;
+            continue;
+        }
+        if (goR) {
+            cur = rc;
+            continue;
+        }
+        bool found = false;
+        while (sp > 0u) {
+            sp -= 1u;
+            uint32_t cand = stk[sp * 128u];
+            float tenter = __uint_as_float(stk[sp * 128u + 64u]);
+            if (!prune || !(tenter > prune_bound(closest))) {
+                cur = cand;
+                found = true;
+                break;
+            }
+        }
+        if (!found) break;
     }
     return any;
 }
@@ -424,19 +519,19 @@ RT_DEV Ray apply_op(f4 op, Ray r) {
 }
 
 // A GEOM or BVH entry (the caller guarantees E is wave-uniform).
-RT_DEV bool entry_geom_hit(const DevScene& S, const DevEntry* E, Ray r, float tmin, float& closest,
+RT_DEV bool entry_geom_hit(const DevScene& S, float delta, const DevEntry* E, Ray r, float tmin, float& closest,
                            uint32_t& hit_code, uint32_t* stk, bool exact) {
     uint32_t ntf = E->ntf;
     for (uint32_t i = 0; i < ntf; ++i) r = apply_op(E->tf[i], r);
-    if (E->kind == rtdev::kEntBvh) return bvh_hit(S, E->payload, r, tmin, closest, hit_code, stk, exact);
+    if (E->kind == rtdev::kEntBvh) return bvh_hit(S, delta, E->payload, r, tmin, closest, hit_code, stk, exact);
     RayD q = to_d(r);
     return leaf_hit(S, E->payload, r, q, tmin, closest, hit_code);
 }
 
 // ConstantMedium::hit (hittable.rs:176-233); draws one U(0,1) once the clamped
 // interval is non-empty, exactly where the reference does.
-RT_DEV bool medium_hit(const DevScene& S, const DevEntry* E, Ray r, float tmin, float tmax, Rng& g, const Key& k,
-                       float& t_out, uint32_t* stk, bool exact) {
+RT_DEV bool medium_hit(const DevScene& S, float delta, const DevEntry* E, Ray r, float tmin, float tmax, Rng& g,
+                       const Key& k, float& t_out, uint32_t* stk, bool exact) {
     uint32_t ntf = E->ntf;
     for (uint32_t i = 0; i < ntf; ++i) r = apply_op(E->tf[i], r);
     const DevEntry* B = S.entries + E->payload;
@@ -452,8 +547,8 @@ RT_DEV bool medium_hit(const DevScene& S, const DevEntry* E, Ray r, float tmin, 
         if (!sphere_select(R, t1 + 0.0001f, kInf, t2)) return false;
     } else {
         uint32_t dummy;
-        if (!entry_geom_hit(S, B, r, -kInf, t1, dummy, stk, exact)) return false;
-        if (!entry_geom_hit(S, B, r, t1 + 0.0001f, t2, dummy, stk, exact)) return false;
+        if (!entry_geom_hit(S, delta, B, r, -kInf, t1, dummy, stk, exact)) return false;
+        if (!entry_geom_hit(S, delta, B, r, t1 + 0.0001f, t2, dummy, stk, exact)) return false;
     }
     if (t1 < tmin) t1 = tmin;
     if (t2 > tmax) t2 = tmax;
@@ -468,15 +563,15 @@ RT_DEV bool medium_hit(const DevScene& S, const DevEntry* E, Ray r, float tmin, 
 }
 
 // HittableList::hit over the world (hittable.rs:100-118), t in [0.001, inf).
-RT_DEV bool world_hit(const DevScene& S, const Ray& r, Rng& g, const Key& k, float& t_hit, uint32_t& hit_entry,
-                      uint32_t& hit_code, uint32_t* stk, bool exact) {
+RT_DEV bool world_hit(const DevScene& S, float delta, const Ray& r, Rng& g, const Key& k, float& t_hit,
+                      uint32_t& hit_entry, uint32_t& hit_code, uint32_t* stk, bool exact) {
     float closest = kInf;
     bool any = false;
     for (uint32_t e = 0; e < S.num_top; ++e) {
         const DevEntry* E = S.entries + e;
         if (E->kind == rtdev::kEntMedium) {
             float t;
-            if (medium_hit(S, E, r, 0.001f, closest, g, k, t, stk, exact)) {
+            if (medium_hit(S, delta, E, r, 0.001f, closest, g, k, t, stk, exact)) {
                 closest = t;
                 hit_entry = e;
                 hit_code = rtdev::leaf_code(rtdev::kLeafMedium, 0);
@@ -484,7 +579,7 @@ RT_DEV bool world_hit(const DevScene& S, const Ray& r, Rng& g, const Key& k, flo
             }
         } else {
             uint32_t code;
-            if (entry_geom_hit(S, E, r, 0.001f, closest, code, stk, exact)) {
+            if (entry_geom_hit(S, delta, E, r, 0.001f, closest, code, stk, exact)) {
                 hit_entry = e;
                 hit_code = code;
                 any = true;
@@ -806,7 +901,7 @@ __global__ __launch_bounds__(64) void trace_samples(DevScene S, DevCamera C, Dev
                                                      unsigned long long* __restrict__ seg_counter) {
     extern __shared__ uint32_t lds_stack[];
     const uint32_t lane = threadIdx.x;
-    uint32_t* stk = lds_stack + lane;
+    uint32_t* stk = lds_stack + lane;  // [level][{node, t_enter}][lane]
     const Key k{P.seed_lo, P.seed_hi};
     const bool exact = (P.flags & RT_FLAG_EXACT_BVH) != 0u;
     const V bg = mk(P.bg[0], P.bg[1], P.bg[2]);
@@ -877,7 +972,7 @@ __global__ __launch_bounds__(64) void trace_samples(DevScene S, DevCamera C, Dev
                 nseg += 1u;
                 float t;
                 uint32_t entry = 0, code = 0;
-                if (!world_hit(S, ray, g, k, t, entry, code, stk, exact)) {
+                if (!world_hit(S, P.prune_delta, ray, g, k, t, entry, code, stk, exact)) {
                     L = L + T * bg;
                     done = true;
                 } else {
@@ -974,6 +1069,7 @@ struct rt_scene {
     uint64_t sbuf_bytes = 0;
     unsigned* counter = nullptr;
     int grid = 0;  // resident waves of trace_samples
+    float coord_bound = 0.0f;
 };
 
 namespace {
@@ -1103,6 +1199,7 @@ int rt_scene_upload(const rt_scene_desc* desc, int device, rt_scene_handle* out)
     d.num_top = hs.num_top;
     d.num_entries = (uint32_t)hs.entries.size();
     d.stack_depth = hs.max_bvh_depth + 1u;
+    s->coord_bound = hs.coord_bound;
     uint64_t c[10] = {hs.entries.size(), hs.sph.size(), hs.msph.size() / 3, hs.rect.size() / 2, hs.tri.size() / 3,
                       hs.nodes.size() / 2, hs.mats.size(), hs.texs.size(), hs.max_bvh_depth, total};
     memcpy(s->counts, c, sizeof c);
@@ -1156,6 +1253,16 @@ int rt_render_launch(rt_scene_handle s, const rt_camera_desc* camera, const rt_r
     dp.bg[0] = p->background[0];
     dp.bg[1] = p->background[1];
     dp.bg[2] = p->background[2];
+    {
+        // Pruning margin: every ray origin and hit point lies within R of the
+        // origin of any BVH frame (camera + lens, scene coordinates, translations).
+        double R = sqrt((double)cam.origin[0] * cam.origin[0] + (double)cam.origin[1] * cam.origin[1] +
+                        (double)cam.origin[2] * cam.origin[2]) +
+                   2.0 * (double)fabsf(cam.lens_radius) + 2.0 * (double)s->coord_bound;
+        double delta = R * (1.0 / 1048576.0) * 1.01 + 1e-30;  // 2^-20 R
+        dp.prune_delta = (float)delta;
+        if (!(dp.prune_delta < 1e30f)) dp.flags |= RT_FLAG_EXACT_BVH;  // non-finite scene: no pruning
+    }
     uint32_t nblk = dp.num_blocks > dp.shard_index ? (dp.num_blocks - dp.shard_index + dp.shard_count - 1u) / dp.shard_count : 0u;
     if (nblk == 0) return RT_OK;
     DeviceGuard g(s->device);
@@ -1183,7 +1290,7 @@ int rt_render_launch(rt_scene_handle s, const rt_camera_desc* camera, const rt_r
         if ((e = hipMalloc(&s->counter, 256)) != hipSuccess)
             return rthost::set_error(RT_ERR_OOM, std::string("hipMalloc counter: ") + hipGetErrorString(e));
     }
-    size_t lds = (size_t)s->dev.stack_depth * 64u * sizeof(uint32_t);
+    size_t lds = (size_t)s->dev.stack_depth * 128u * sizeof(uint32_t);
     if (s->grid == 0) {
         int per_cu = 0, cus = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace_samples, 64, lds) != hipSuccess || per_cu < 1)

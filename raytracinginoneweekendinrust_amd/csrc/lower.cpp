@@ -16,6 +16,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <cmath>
 #include <functional>
 #include <unordered_map>
 
@@ -386,7 +387,25 @@ class Lowerer {
         return id;
     }
 
+    void note_coords(const rt_node& n) {
+        float m = 0.0f;
+        const float* f = n.f;
+        auto upd = [&](float v) {
+            v = v < 0.0f ? -v : v;
+            if (v > m || v != v) m = v != v ? 3.0e38f : v;
+        };
+        switch (n.kind) {
+            case RT_OBJ_SPHERE: for (int i = 0; i < 3; ++i) upd(std::fabs(f[i]) + std::fabs(f[3])); break;
+            case RT_OBJ_MOVING_SPHERE:
+                for (int i = 0; i < 6; ++i) upd(std::fabs(f[i]) + std::fabs(f[8]));
+                break;
+            default: for (int i = 0; i < 9; ++i) upd(f[i]); break;
+        }
+        if (m > s_->coord_bound) s_->coord_bound = m;
+    }
+
     int lower_prim(int idx, uint32_t* code) {
+        note_coords(node(idx));
         auto it = prim_memo_.find(idx);
         if (it != prim_memo_.end()) {
             *code = it->second;
@@ -485,6 +504,7 @@ class Lowerer {
         if (rc) return rc;
         if (count == 0) return fail(RT_ERR_INVALID, "BVH over an empty list");
         std::vector<LeafInfo> items(count);
+        bool prunable = true;  // closest-hit pruning is proven safe only for these leaf types
         for (uint32_t i = 0; i < count; ++i) {
             int ni = d_->list_items[first + i];
             if (!valid(ni)) return fail(RT_ERR_INVALID, "list item out of range");
@@ -493,6 +513,7 @@ class Lowerer {
                 return fail(RT_ERR_UNSUPPORTED, "device BVH leaves must be Sphere/MovingSphere/Rect/Cube/Tri (node " +
                                                     std::to_string(ni) + " kind " + std::to_string(c.kind) + ")");
             if ((rc = lower_prim(ni, &items[i].code))) return rc;
+            if (c.kind == RT_OBJ_MOVING_SPHERE || c.kind == RT_OBJ_TRI) prunable = false;
             items[i].box01 = prim_box(c, n.f[0], n.f[1]);
             Box b00 = prim_box(c, 0.0f, 0.0f);  // box_compare uses bounding_box(0.0, 0.0), bvh.rs:421-422
             items[i].key[0] = b00.mn.x;
@@ -537,10 +558,15 @@ class Lowerer {
             return (uint32_t)tn.size() - 1;
         };
         uint32_t troot = helper(items.data(), count, 1);
-        // Flatten in DFS preorder.
-        uint32_t base = (uint32_t)(s_->nodes.size() / 2);
+        // Flatten to BVH2 nodes that carry both children's boxes (64 B each), in DFS
+        // preorder, behind a wrapper node whose single child is the root (so the
+        // root's box is tested on entry, as bvh.rs:370 does). Leaf children carry
+        // their DFS ordinal ("rank", cube faces rank + 0..5): the device may visit
+        // children nearest-first and still resolves equal-t ties like the
+        // reference's recursion (later in DFS order wins, bvh.rs:406-414).
+        uint32_t base = (uint32_t)(s_->nodes.size() / 4);
         std::vector<uint32_t> remap(tn.size());
-        uint32_t next = base;
+        uint32_t next = base + 1;
         std::function<void(uint32_t)> order = [&](uint32_t i) {
             remap[i] = next++;
             for (int k = 0; k < 2; ++k)
@@ -548,16 +574,40 @@ class Lowerer {
         };
         order(troot);
         if (next > rtdev::kMaxIndex) return fail(RT_ERR_UNSUPPORTED, "too many BVH nodes");
-        s_->nodes.resize((size_t)next * 2);
+        s_->nodes.resize((size_t)next * 4);
+        std::vector<uint32_t> rank(tn.size() * 2, 0);
+        uint32_t ordinal = 0;
+        std::function<void(uint32_t)> ranks = [&](uint32_t i) {
+            for (int k = 0; k < 2; ++k) {
+                if (tn[i].is_node[k]) ranks(tn[i].child[k]);
+                else if (tn[i].child[k] != rtdev::kChildEmpty) rank[2 * i + k] = (++ordinal) * 8u;
+            }
+        };
+        ranks(troot);
+        auto put = [&](uint32_t o, const Box& lb, const Box& rb, uint32_t lc, uint32_t rc, uint32_t lr, uint32_t rr) {
+            s_->nodes[4 * (size_t)o + 0] = {lb.mn.x, lb.mn.y, lb.mn.z, lb.mx.x};
+            s_->nodes[4 * (size_t)o + 1] = {lb.mx.y, lb.mx.z, rb.mn.x, rb.mn.y};
+            s_->nodes[4 * (size_t)o + 2] = {rb.mn.z, rb.mx.x, rb.mx.y, rb.mx.z};
+            s_->nodes[4 * (size_t)o + 3] = {bitsf(lc), bitsf(rc), bitsf(lr), bitsf(rr)};
+        };
+        const Box none{{0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f}};
+        put(base, tn[troot].box, none, remap[troot], rtdev::kChildEmpty, prunable ? rtdev::kBvhPrunable : 0u, 0u);
         for (uint32_t i = 0; i < tn.size(); ++i) {
-            uint32_t o = remap[i];
-            uint32_t l = tn[i].is_node[0] ? remap[tn[i].child[0]] : tn[i].child[0];
-            uint32_t r = tn[i].is_node[1] ? remap[tn[i].child[1]] : tn[i].child[1];
-            s_->nodes[2 * o] = {tn[i].box.mn.x, tn[i].box.mn.y, tn[i].box.mn.z, bitsf(l)};
-            s_->nodes[2 * o + 1] = {tn[i].box.mx.x, tn[i].box.mx.y, tn[i].box.mx.z, bitsf(r)};
+            Box cb[2];
+            uint32_t cc[2];
+            for (int k = 0; k < 2; ++k) {
+                if (tn[i].is_node[k]) {
+                    cb[k] = tn[tn[i].child[k]].box;
+                    cc[k] = remap[tn[i].child[k]];
+                } else {
+                    cb[k] = none;
+                    cc[k] = tn[i].child[k];
+                }
+            }
+            put(remap[i], cb[0], cb[1], cc[0], cc[1], rank[2 * i], rank[2 * i + 1]);
         }
-        s_->max_bvh_depth = std::max(s_->max_bvh_depth, max_depth_);
-        *root_out = remap[troot];
+        s_->max_bvh_depth = std::max(s_->max_bvh_depth, max_depth_ + 1);
+        *root_out = base;
         return RT_OK;
     }
 
@@ -585,6 +635,7 @@ class Lowerer {
                     return fail(RT_ERR_UNSUPPORTED, "more than 3 nested Translate/RotateY");
                 Chain c2 = chain;
                 if (n.kind == RT_OBJ_TRANSLATE) {
+                    translate_sum_ += std::fabs(n.f[0]) + std::fabs(n.f[1]) + std::fabs(n.f[2]);
                     c2.op[c2.n++] = {n.f[0], n.f[1], n.f[2], 0.0f};
                 } else {
                     float radians = rt_to_radians(n.f[0]);  // instance.rs:64-67
@@ -629,6 +680,10 @@ class Lowerer {
     std::vector<rtdev::DevEntry> aux_;
     std::unordered_map<int, uint32_t> tex_memo_, mat_memo_, prim_memo_, phase_memo_;
     uint32_t max_depth_ = 0;
+    float translate_sum_ = 0.0f;
+
+   public:
+    float translate_sum() const { return translate_sum_; }
 };
 
 }  // namespace
@@ -636,7 +691,9 @@ class Lowerer {
 int lower_scene(const rt_scene_desc* desc, HostScene* out, std::string* err) {
     *out = HostScene();
     Lowerer l(desc, out, err);
-    return l.run();
+    int rc = l.run();
+    out->coord_bound += l.translate_sum();
+    return rc;
 }
 
 }  // namespace rthost

@@ -22,6 +22,9 @@ struct HostScene {
     std::vector<rtdev::DevTexture> texs;
     std::vector<uint8_t> perm, texels;
     uint32_t max_bvh_depth = 0;  // internal levels of the deepest BVH
+    // Upper bound on |coordinate| of any primitive in any instance frame plus the
+    // translations applied to reach it (bounds ray lengths for the pruning margin).
+    float coord_bound = 0.0f;
     uint64_t bytes() const;
 };
 

@@ -212,3 +212,20 @@ def test_c3_full_workload_subsample_matches_oracle(rt, orc):
     assert mask.sum() > 3000
     np.testing.assert_array_equal(got[mask], want[mask])
     assert np.isfinite(got).all()
+
+
+@pytest.mark.parametrize("cfg_name,spp", [("C3", 24), ("C2", 8), ("C1", 16)])
+def test_pruned_traversal_equals_reference_traversal_full_frame(cfg_name, spp, rt):
+    # Closest-hit box pruning must not change a single path: same bits AND the
+    # same number of ray segments as the reference's unpruned traversal.
+    cfg = rt.CONFIGS[cfg_name]
+    cfg = cfg.scaled(cfg.width, spp)
+    scene = rt.Scene.generate(cfg.scene, cfg.scene_seed)
+    ds = rt.DeviceScene(scene)
+    out = {}
+    for exact in (True, False):
+        p = rt.render_params(cfg.width, cfg.height, cfg.spp, cfg.depth, background=cfg.background(), exact_bvh=exact)
+        out[exact] = ds.render(cfg.camera(), p)
+    ds.close()
+    np.testing.assert_array_equal(out[True][0], out[False][0])
+    assert out[True][1]["segments"] == out[False][1]["segments"]
