@@ -41,8 +41,11 @@ def log(*a):
 
 
 def bytes_per_sample(counters: dict, spp: int) -> float:
+    """Algorithmic bytes per camera sample of trace_samples: the scene records the
+    reference algorithm touches (counted by the oracle) + the 12-byte radiance
+    record each sample writes to the HBM sample buffer + 12/spp framebuffer."""
     total = sum(BYTES[k] * counters[k] for k in BYTES)
-    return total / counters["samples"] + 12.0 / spp
+    return total / counters["samples"] + 12.0 + 12.0 / spp
 
 
 def cpu_threads() -> int:
@@ -53,26 +56,39 @@ def cpu_threads() -> int:
     return max(1, n)
 
 
-def oracle_measure(cfg, scene, target_s: float, threads: int):
-    """Oracle render of a block subsample of the config at full spp/depth: the CPU
-    baseline (Msamples/s on `threads` host threads) and the per-sample counts for
-    the roofline's algorithmic bytes."""
+SUBSAMPLE = 64  # counts from a fixed 1/64 subsample at the config's spp and depth
+
+
+def oracle_measure(cfg, scene, threads: int):
+    """Oracle render of the fixed 1/64 block subsample (8x8 blocks b with
+    b % 64 == 21, spread over the whole frame) at full spp/depth: the CPU baseline
+    (Msamples/s on `threads` host threads) and the reference algorithm's per-sample
+    counts for the roofline's algorithmic bytes."""
     import oracle_ffi as orc
     import raytracinginoneweekendinrust_amd as rt
-    cam = cfg.camera()
-    bg = cfg.background()
-    nblocks = ((cfg.width + 7) // 8) * ((cfg.height + 7) // 8)
-    k = 4096
-    p = rt.render_params(cfg.width, cfg.height, cfg.spp, cfg.depth, background=bg, shard_index=k // 3,
-                         shard_count=k, seed=cfg.render_seed)
-    _, cal = orc.render(scene, cam, p, threads=threads)
-    rate = cal["samples"] / max(cal["seconds"], 1e-6)
-    want = max(1, int(rate * target_s / (64 * cfg.spp)))  # blocks to render
-    k2 = max(1, min(k, nblocks // want))
-    p = rt.render_params(cfg.width, cfg.height, cfg.spp, cfg.depth, background=bg, shard_index=(k2 // 3) % k2,
-                         shard_count=k2, seed=cfg.render_seed)
-    _, cnt = orc.render(scene, cam, p, threads=threads)
-    return cnt, k2
+    p = rt.render_params(cfg.width, cfg.height, cfg.spp, cfg.depth, background=cfg.background(), shard_index=21,
+                         shard_count=SUBSAMPLE, seed=cfg.render_seed)
+    _, cnt = orc.render(scene, cfg.camera(), p, threads=threads)
+    return cnt
+
+
+def rank_work(rt, cfg, rank: int, world: int, scaling: str, exact_bvh: bool = False):
+    """The multi-GPU decomposition: render params of `rank` and its
+    pixel count. weak: every rank renders the whole frame with samples
+    [rank*spp, (rank+1)*spp); strong: 8x8 blocks b with b % world == rank."""
+    W, H, spp = cfg.width, cfg.height, cfg.spp
+    if scaling == "weak":
+        params = rt.render_params(W, H, spp, cfg.depth, background=cfg.background(), seed=cfg.render_seed,
+                                  sample_base=rank * spp, exact_bvh=exact_bvh)
+        return params, W * H
+    params = rt.render_params(W, H, spp, cfg.depth, background=cfg.background(), seed=cfg.render_seed,
+                              shard_index=rank, shard_count=world, exact_bvh=exact_bvh)
+    bx, by = (W + 7) // 8, (H + 7) // 8
+    pixels = 0
+    for b in range(rank, bx * by, world):
+        x0, y0 = (b % bx) * 8, (b // bx) * 8
+        pixels += (min(W, x0 + 8) - x0) * (min(H, y0 + 8) - y0)
+    return params, pixels
 
 
 def main() -> int:
@@ -83,7 +99,6 @@ def main() -> int:
     ap.add_argument("--config", default="C3")
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--exact-bvh", action="store_true")
     args = ap.parse_args()
 
@@ -110,15 +125,7 @@ def main() -> int:
     ds = rt.DeviceScene(scene, device=local_rank)
     cam = cfg.camera()
     W, H, spp = cfg.width, cfg.height, cfg.spp
-    if args.scaling == "weak":
-        params = rt.render_params(W, H, spp, cfg.depth, background=cfg.background(), seed=cfg.render_seed,
-                                  sample_base=rank * spp, exact_bvh=args.exact_bvh)
-        pixels_rank = W * H
-    else:
-        params = rt.render_params(W, H, spp, cfg.depth, background=cfg.background(), seed=cfg.render_seed,
-                                  shard_index=rank, shard_count=world, exact_bvh=args.exact_bvh)
-        bx = (W + 7) // 8
-        pixels_rank = sum(1 for y in range(H) for x in range(W) if ((y // 8) * bx + x // 8) % world == rank)
+    params, pixels_rank = rank_work(rt, cfg, rank, world, args.scaling, args.exact_bvh)
     out = torch.zeros(W * H * 3, dtype=torch.float32, device="cuda")
     seg = torch.zeros(1, dtype=torch.int64, device="cuda")
     stream = torch.cuda.current_stream()
@@ -129,6 +136,7 @@ def main() -> int:
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    ds.trace_time(reset=True)  # drop warmup launches from the per-launch timing
     seg.zero_()
     if world > 1:
         dist.barrier()
@@ -145,7 +153,9 @@ def main() -> int:
         dist.barrier()
     t1 = time.perf_counter()
     wall = t1 - t0
-    kernel_ms = ev0.elapsed_time(ev1) / args.steps
+    step_ms = ev0.elapsed_time(ev1) / args.steps          # device time of a whole step (all kernels)
+    trace_total_ms, trace_launches = ds.trace_time(reset=True)  # HIP events around each trace_samples launch
+    kernel_ms = trace_total_ms / max(trace_launches, 1)
     segments = int(seg.item())
     t = torch.tensor([wall, float(segments)], dtype=torch.float64, device="cuda")
     if world > 1:
@@ -164,20 +174,19 @@ def main() -> int:
         threads = cpu_threads()
         cpu = None
         try:
+            cnt = oracle_measure(cfg, scene, threads)
             if world == 1 and not args.no_cpu_baseline:
-                cnt, k2 = oracle_measure(cfg, scene, args.cpu_seconds, threads)
                 cpu = {"value": cnt["samples"] / cnt["seconds"] / 1e6, "unit": "Msamples/s", "cores": cnt["threads"],
                        "kind": "port",
-                       "sample": f"{cfg.name} 8x8 blocks b % {k2} == {(k2 // 3) % k2} ({cnt['samples'] // spp} px) "
-                                 f"at {spp} spp depth {cfg.depth}, {cnt['samples']} samples in {cnt['seconds']:.1f}s "
-                                 f"(C oracle, pthreads)"}
-            else:
-                cnt, _ = oracle_measure(cfg, scene, 1.0, threads)
+                       "sample": f"{cfg.name} 8x8 blocks b % {SUBSAMPLE} == 21 ({cnt['samples'] // spp} px, 1/64 of "
+                                 f"the frame) at {spp} spp depth {cfg.depth}: {cnt['samples']} samples in "
+                                 f"{cnt['seconds']:.1f}s (C oracle, pthreads)"}
         except Exception as e:  # the oracle is optional on the box; the product path is not
             log(f"oracle unavailable: {e}")
             cnt = None
         b_sample = bytes_per_sample(cnt, spp) if cnt else None
-        achieved = (b_sample * samples_rank_launch / (kernel_ms / 1e3) / 1e9) if b_sample else None
+        samples_per_trace_launch = samples_rank_launch * args.steps / max(trace_launches, 1)
+        achieved = (b_sample * samples_per_trace_launch / (kernel_ms / 1e3) / 1e9) if b_sample else None
         traffic = None
         pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
         if os.path.exists(pmc):
@@ -211,8 +220,9 @@ def main() -> int:
             "image_finite": img_ok,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
-                         "kernel_ms": kernel_ms, "bytes_per_sample": b_sample,
-                         "samples_per_launch": samples_rank_launch},
+                         "kernel": "trace_samples", "kernel_ms": kernel_ms, "launches_per_step":
+                             trace_launches / args.steps, "step_device_ms": step_ms,
+                         "bytes_per_sample": b_sample, "samples_per_launch": samples_per_trace_launch},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -166,6 +166,11 @@ int rt_render_launch(rt_scene_handle scene, const rt_camera_desc* camera,
                      const rt_render_params* params, float* d_out,
                      unsigned long long* d_segments, void* stream);
 
+/* Device time of the trace kernel launches issued by rt_render_launch on this
+ * scene since the last reset (HIP events recorded on the launch stream around
+ * each launch; waits for them). Up to 256 launches are kept between resets. */
+int rt_scene_trace_time(rt_scene_handle scene, double* total_ms, uint64_t* launches, int reset);
+
 /* Synchronous drop-in for Renderer::render minus the PPM write: renders into a
  * HOST buffer of W*H*3 floats (pixels outside the shard are left untouched). */
 int rt_render(rt_scene_handle scene, const rt_camera_desc* camera,

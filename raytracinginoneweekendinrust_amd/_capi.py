@@ -72,6 +72,7 @@ SIGNATURES = [
     ("rt_scene_info", C.c_int, [C.c_void_p, C.POINTER(C.c_uint64)]),
     ("rt_render_launch", C.c_int, [C.c_void_p, C.POINTER(rt_camera_desc), C.POINTER(rt_render_params), C.c_void_p,
                                    C.c_void_p, C.c_void_p]),
+    ("rt_scene_trace_time", C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_uint64), C.c_int]),
     ("rt_render", C.c_int, [C.c_void_p, C.POINTER(rt_camera_desc), C.POINTER(rt_render_params),
                             C.POINTER(C.c_float), C.POINTER(rt_stats)]),
     ("rt_scene_generate", C.c_int, [C.c_char_p, C.c_uint64, C.c_char_p, C.POINTER(C.POINTER(rt_scene_desc))]),

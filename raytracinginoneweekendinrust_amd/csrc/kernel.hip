@@ -1070,6 +1070,11 @@ struct rt_scene {
     unsigned* counter = nullptr;
     int grid = 0;  // resident waves of trace_samples
     float coord_bound = 0.0f;
+    // HIP events bracketing every trace_samples launch (rt_scene_trace_time)
+    static constexpr int kEvents = 256;
+    hipEvent_t ev[kEvents][2] = {};
+    int ev_count = 0;
+    bool ev_overflow = false;
 };
 
 namespace {
@@ -1215,6 +1220,9 @@ int rt_scene_free(rt_scene_handle s) {
         if (s->pool) (void)hipFree(s->pool);
         if (s->sbuf) (void)hipFree(s->sbuf);
         if (s->counter) (void)hipFree(s->counter);
+        for (int i = 0; i < rt_scene::kEvents; ++i)
+            for (int j = 0; j < 2; ++j)
+                if (s->ev[i][j]) (void)hipEventDestroy(s->ev[i][j]);
     }
     delete s;
     return RT_OK;
@@ -1270,7 +1278,7 @@ int rt_render_launch(rt_scene_handle s, const rt_camera_desc* camera, const rt_r
     // Sample buffer: chunks of whole sample ranges (the per-pixel sum stays in order).
     const uint64_t npix = (uint64_t)p->width * p->height;
     const uint64_t per_sample = npix * 3u * sizeof(float);
-    uint64_t budget = 4096ull << 20;
+    uint64_t budget = 8192ull << 20;
     if (const char* env = getenv("RT_SAMPLE_BUFFER_MB")) budget = strtoull(env, nullptr, 10) << 20;
     uint64_t max_s = budget / per_sample;
     if (max_s < 1) max_s = 1;
@@ -1310,9 +1318,22 @@ int rt_render_launch(rt_scene_handle s, const rt_camera_desc* camera, const rt_r
         if ((e = hipMemsetAsync(s->counter, 0, sizeof(unsigned), st)) != hipSuccess) return hip_fail(e, "memset counter");
         uint32_t grid = (uint32_t)s->grid;
         if (grid > q.num_batches) grid = q.num_batches;
+        hipEvent_t* evp = nullptr;
+        if (s->ev_count < rt_scene::kEvents) {
+            evp = s->ev[s->ev_count];
+            for (int j = 0; j < 2; ++j)
+                if (!evp[j] && hipEventCreate(&evp[j]) != hipSuccess) evp = nullptr;
+        } else {
+            s->ev_overflow = true;
+        }
+        if (evp) (void)hipEventRecord(evp[0], st);
         hipLaunchKernelGGL(trace_samples, dim3(grid), dim3(64), lds, st, s->dev, cam, dp, q, s->sbuf, s->counter,
                            d_segments);
         if ((e = hipGetLastError()) != hipSuccess) return hip_fail(e, "trace_samples launch");
+        if (evp) {
+            (void)hipEventRecord(evp[1], st);
+            s->ev_count++;
+        }
         hipLaunchKernelGGL(resolve_samples, dim3((uint32_t)((npix + 255u) / 256u)), dim3(256), 0, st, s->sbuf, d_out, dp,
                            q, c == 0 ? 1 : 0, c + 1 == nchunks ? 1 : 0);
         if ((e = hipGetLastError()) != hipSuccess) return hip_fail(e, "resolve_samples launch");
@@ -1370,6 +1391,31 @@ int rt_render(rt_scene_handle s, const rt_camera_desc* camera, const rt_render_p
         stats->kernel_ms = ms;
     }
     cleanup();
+    return RT_OK;
+}
+
+int rt_scene_trace_time(rt_scene_handle s, double* total_ms, uint64_t* launches, int reset) {
+    rthost::clear_error();
+    if (!s || !total_ms || !launches) return rthost::set_error(RT_ERR_INVALID, "NULL argument");
+    DeviceGuard g(s->device);
+    double sum = 0.0;
+    for (int i = 0; i < s->ev_count; ++i) {
+        hipError_t e = hipEventSynchronize(s->ev[i][1]);
+        if (e != hipSuccess) return hip_fail(e, "hipEventSynchronize");
+        float ms = 0.0f;
+        if ((e = hipEventElapsedTime(&ms, s->ev[i][0], s->ev[i][1])) != hipSuccess) return hip_fail(e, "hipEventElapsedTime");
+        sum += ms;
+    }
+    *total_ms = sum;
+    *launches = (uint64_t)s->ev_count;
+    if (s->ev_overflow) {
+        if (reset) {
+            s->ev_count = 0;
+            s->ev_overflow = false;
+        }
+        return rthost::set_error(RT_ERR_INVALID, "more than 256 launches since the last reset: timing incomplete");
+    }
+    if (reset) s->ev_count = 0;
     return RT_OK;
 }
 
