@@ -10,7 +10,8 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_DIR = os.path.join(_HERE, "_lib")
-LIB_PATH = os.path.join(LIB_DIR, "librtamd.so")
+# RT_LIBRARY selects a diagnostic build of the same ABI (e.g. _lib/librtamd_prof.so, tools/region_profile.py).
+LIB_PATH = os.environ.get("RT_LIBRARY") or os.path.join(LIB_DIR, "librtamd.so")
 ASSET_DIR = os.path.normpath(os.path.join(_HERE, "..", "assets"))
 
 # rt_node_kind

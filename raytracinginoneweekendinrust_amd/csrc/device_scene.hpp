@@ -130,6 +130,7 @@ struct DevParams {
     uint32_t flags;
     float bg[3];
     float prune_delta;  // box inflation for closest-hit pruning ("exact pruning")
+    uint32_t tune;      // kMode* traversal switches from RT_TUNE (diagnostics)
 };
 
 }  // namespace rtdev

@@ -20,6 +20,7 @@
 // has no dense contraction.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
@@ -46,6 +47,54 @@ using rtdev::f4;
 namespace {
 
 constexpr float kInf = __builtin_inff();
+
+// ---------------------------------------------------------------------------
+// Region profiler (diagnostic build only: -DRT_PROFILE_REGIONS -> librtamd_prof.so,
+// see tools/region_profile.py). Per region: wave cycles (s_memtime), wave
+// executions and active lanes at region end; accumulated per wave in LDS by the
+// first active lane, flushed to g_prof once per wave. Compiles to nothing in the
+// product library.
+// ---------------------------------------------------------------------------
+enum ProfRegion : uint32_t {
+    kPrRefill = 0, kPrSegment, kPrWorld, kPrRecord, kPrEmit, kPrScatter, kPrMarble, kPrStore,
+    kPrChecker, kPrImage, kPrUnitSphere, kPrDielectric, kPrLambert, kPrMetal, kPrIso, kPrLog,
+    kPrEntry0 = 16, kPrWfShade = 32, kPrWfRegen, kPrWfInline, kPrWfTail, kPrWfLogicWave, kPrWfPassWave,
+    kPrWfBvhStart, kPrWfBvhRefill, kPrWfBvhWave, kPrWfLoad, kPrBvhTrip = 44, kPrLeafTest = 45, kPrCount = 48
+};
+// traversal mode bits (bvh_hit): kModeExact = RT_FLAG_EXACT_BVH; the rest come
+// from DevParams::tune (RT_TUNE environment variable, diagnostics / A-B runs).
+constexpr uint32_t kModeExact = 1u, kModeNoLeafBoxes = 2u, kModeWavefront = 4u;
+#ifdef RT_PROFILE_REGIONS
+constexpr uint32_t kProfCopies = 64;  // flush targets spread over blockIdx to keep atomics uncontended
+__device__ unsigned long long g_prof[kProfCopies * 3 * kPrCount];
+__shared__ unsigned long long prof_lds[3 * kPrCount];
+__device__ __forceinline__ void prof_init() {
+    for (uint32_t i = threadIdx.x; i < 3u * kPrCount; i += blockDim.x) prof_lds[i] = 0u;
+}
+__device__ __forceinline__ void prof_flush() {
+    unsigned long long* dst = g_prof + (blockIdx.x % kProfCopies) * 3u * kPrCount;
+    for (uint32_t i = threadIdx.x; i < 3u * kPrCount; i += blockDim.x)
+        if (prof_lds[i]) atomicAdd(&dst[i], prof_lds[i]);
+}
+#define PROF_T0(name) const uint64_t name = __builtin_amdgcn_s_memtime()
+#define PROF_ADD(region, t0) prof_add((region), (t0))
+__device__ __forceinline__ void prof_add(uint32_t region, uint64_t t0) {
+    uint64_t dt = __builtin_amdgcn_s_memtime() - t0;
+    uint64_t m = __ballot(1);
+    if (__lane_id() == (uint32_t)__builtin_ctzll(m)) {
+        prof_lds[region] += dt;
+        prof_lds[kPrCount + region] += 1u;
+        prof_lds[2 * kPrCount + region] += (uint64_t)__popcll(m);
+    }
+}
+#define PROF_INIT() prof_init()
+#define PROF_FLUSH() prof_flush()
+#else
+#define PROF_T0(name) do { } while (0)
+#define PROF_ADD(region, t0) do { } while (0)
+#define PROF_INIT() do { } while (0)
+#define PROF_FLUSH() do { } while (0)
+#endif
 
 // ---------------------------------------------------------------------------
 // vector math, glam 0.22 evaluation order
@@ -255,14 +304,18 @@ RT_DEV bool msphere_t(f4 m0, f4 m1, f4 m2, const Ray& r, float tmin, float tmax,
 }
 
 // rectangle.rs:36-65 / 98-127 / 160-189; axis 0 = XY (plane z), 1 = XZ (plane y), 2 = YZ (plane x)
+// Selects between values, never between addresses (a select of struct-member
+// addresses pins the struct in scratch memory).
+RT_DEV float sel3(uint32_t axis, float v0, float v1, float v2) { return axis == 0u ? v0 : (axis == 1u ? v1 : v2); }
 RT_DEV void rect_axes(uint32_t axis, const Ray& r, float& ok, float& dk, float& oa, float& da, float& ob,
                       float& db) {
-    ok = axis == 0u ? r.o.z : (axis == 1u ? r.o.y : r.o.x);
-    dk = axis == 0u ? r.d.z : (axis == 1u ? r.d.y : r.d.x);
-    oa = axis == 2u ? r.o.y : r.o.x;
-    da = axis == 2u ? r.d.y : r.d.x;
-    ob = axis == 0u ? r.o.y : r.o.z;
-    db = axis == 0u ? r.d.y : r.d.z;
+    const float ox = r.o.x, oy = r.o.y, oz = r.o.z, dx = r.d.x, dy = r.d.y, dz = r.d.z;
+    ok = sel3(axis, oz, oy, ox);
+    dk = sel3(axis, dz, dy, dx);
+    oa = sel3(axis, ox, ox, oy);
+    da = sel3(axis, dx, dx, dy);
+    ob = sel3(axis, oy, oz, oz);
+    db = sel3(axis, dy, dz, dz);
 }
 RT_DEV bool rect_t(f4 r0, f4 r1, const Ray& r, float tmin, float tmax, float& t) {
     float ok, dk, oa, da, ob, db;
@@ -429,6 +482,41 @@ RT_DEV float slab_entry_inflated(float x0, float y0, float z0, float x1, float y
 // candidate inside it would then compute t > closest (exact pruning).
 RT_DEV float prune_bound(float closest) { return closest + __builtin_fabsf(closest) * 0x1p-19f; }
 
+// Conservative leaf test (prunable BVHs only): false only when the leaf's
+// primitive provably has no hit in [tmin, closest]. The box is the primitive's
+// own bounding box inflated by delta; any computed hit t lies on the ray within
+// rounding distance (<< delta) of that box, and the slab values carry <= 3
+// relative roundings, so the 2^-19 slacks below cover them ("exact
+// pruning"). NaN slab values (0 * inf) never reject.
+RT_DEV bool leaf_box_may_hit(float x0, float y0, float z0, float x1, float y1, float z1, const Ray& r, V inv,
+                             float tmin, float closest, float delta) {
+    float lo = -kInf, hi = kInf;
+    {
+        float a = ((x0 - delta) - r.o.x) * inv.x, b = ((x1 + delta) - r.o.x) * inv.x;
+        bool sw = inv.x < 0.0f;
+        float n = sw ? b : a, f = sw ? a : b;
+        lo = n > lo ? n : lo;
+        hi = f < hi ? f : hi;
+    }
+    {
+        float a = ((y0 - delta) - r.o.y) * inv.y, b = ((y1 + delta) - r.o.y) * inv.y;
+        bool sw = inv.y < 0.0f;
+        float n = sw ? b : a, f = sw ? a : b;
+        lo = n > lo ? n : lo;
+        hi = f < hi ? f : hi;
+    }
+    {
+        float a = ((z0 - delta) - r.o.z) * inv.z, b = ((z1 + delta) - r.o.z) * inv.z;
+        bool sw = inv.z < 0.0f;
+        float n = sw ? b : a, f = sw ? a : b;
+        lo = n > lo ? n : lo;
+        hi = f < hi ? f : hi;
+    }
+    if (lo > prune_bound(closest)) return false;
+    if (tmin > 0.0f && hi < tmin * (1.0f - 0x1p-19f)) return false;
+    return !(lo - hi > (__builtin_fabsf(lo) + __builtin_fabsf(hi)) * 0x1p-19f);
+}
+
 // Bvh::hit / BvhNode::hit (bvh.rs:212-217, 363-417) as an iterative traversal of
 // BVH2 nodes. Every child box gets the reference's own test (stored box, the
 // t_max the BVH was entered with), so no node outside the reference's visit set
@@ -438,72 +526,116 @@ RT_DEV float prune_bound(float closest) { return closest + __builtin_fabsf(close
 // provably holds no candidate that could beat (closest, rank). Children are
 // visited nearest-first; ties resolve by DFS rank exactly like the recursion.
 // The stack lives in LDS, lane-strided: stack[level * 128 + {0, 64} + lane].
-RT_DEV bool bvh_hit(const DevScene& S, float delta, uint32_t root, const Ray& r, float tmin, float& closest,
-                    uint32_t& hit_code, uint32_t* stk, bool exact) {
-    const float tmax_entry = closest;
-    const bool prune = !exact && (__float_as_uint(S.nodes[4 * (size_t)root + 3].z) & rtdev::kBvhPrunable) != 0u;
-    V inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
-    RayD q = to_d(r);
-    bool any = false;
-    uint32_t best_rank = 0, sp = 0, cur = root;
-    for (;;) {
-        const f4* nd = S.nodes + 4 * (size_t)cur;
-        f4 n0 = ld4(nd), n1 = ld4(nd + 1), n2 = ld4(nd + 2), n3 = ld4(nd + 3);
-        uint32_t lc = __float_as_uint(n3.x), rc = __float_as_uint(n3.y);
-        bool goL = false, goR = false;
-        float tl = 0.0f, tr = 0.0f;
-        if (lc & rtdev::kLeafBit) {
-            leaf_hit_ranked(S, lc, __float_as_uint(n3.z), r, q, tmin, closest, best_rank, hit_code, any);
+//
+// The traversal is a resumable state machine (trav_init / trav_step, one node
+// per step) so the wavefront BVH kernel can interleave many rays per lane.
+struct Trav {
+    Ray r;
+    V inv;
+    RayD q;
+    float tmin, tmax_entry, closest;
+    uint32_t best_rank, hit_code, sp, cur;
+    bool any, prune, leaf_boxes;
+};
+// closest / best_rank: the candidate to beat; best_rank = 0 lets an equal-t leaf
+// win (the BVH comes later in list order), ~0u makes it lose.
+// wrapper = the BVH's wrapper node (holds the prunable flag); start = first node
+// to visit (the wrapper itself, or its child once the root box test passed).
+RT_DEV void trav_init(Trav& T, const DevScene& S, uint32_t wrapper, uint32_t start, const Ray& r, float tmin,
+                      float tmax_entry, float closest, uint32_t best_rank, uint32_t mode) {
+    T.r = r;
+    T.inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
+    T.q = to_d(r);
+    T.tmin = tmin;
+    T.tmax_entry = tmax_entry;
+    T.closest = closest;
+    T.best_rank = best_rank;
+    T.hit_code = 0u;
+    T.sp = 0u;
+    T.cur = start;
+    T.any = false;
+    T.prune = !(mode & kModeExact) && (__float_as_uint(S.nodes[4 * (size_t)wrapper + 3].z) & rtdev::kBvhPrunable) != 0u;
+    T.leaf_boxes = T.prune && !(mode & kModeNoLeafBoxes);
+}
+// Visits node T.cur; returns false once the traversal is complete. The two
+// children go through one loop (not unrolled) so the leaf tests exist once in
+// the code: inlining them per child doubled the kernel's register footprint.
+RT_DEV bool trav_step(Trav& T, const DevScene& S, float delta, uint32_t* stk) {
+    // by-value copies: a select between struct members (rect_axes) would
+    // otherwise become a select of addresses and pin T in scratch memory
+    const Ray r = T.r;
+    const V inv = T.inv;
+    const RayD q = T.q;
+    const f4* nd = S.nodes + 4 * (size_t)T.cur;
+    f4 n0 = ld4(nd), n1 = ld4(nd + 1), n2 = ld4(nd + 2), n3 = ld4(nd + 3);
+    const uint32_t lc = __float_as_uint(n3.x), rc = __float_as_uint(n3.y);
+    bool goL = false, goR = false;
+    float tl = 0.0f, tr = 0.0f;
+    PROF_T0(pt);
+#pragma unroll 1
+    for (uint32_t k = 0; k < 2u; ++k) {
+        const uint32_t c = k ? rc : lc;
+        if (c == rtdev::kChildEmpty) continue;
+        float x0 = k ? n1.z : n0.x, y0 = k ? n1.w : n0.y, z0 = k ? n2.x : n0.z;
+        float x1 = k ? n2.y : n0.w, y1 = k ? n2.z : n1.x, z1 = k ? n2.w : n1.y;
+        if (c & rtdev::kLeafBit) {
+            if (!T.leaf_boxes || leaf_box_may_hit(x0, y0, z0, x1, y1, z1, r, inv, T.tmin, T.closest, delta)) {
+                PROF_T0(pl);
+                leaf_hit_ranked(S, c, __float_as_uint(k ? n3.w : n3.z), r, q, T.tmin, T.closest, T.best_rank,
+                                T.hit_code, T.any);
+                PROF_ADD(kPrLeafTest, pl);
+            }
         } else {
-            goL = slab(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, r, inv, tmin, tmax_entry, tl);
-            if (goL && prune) {
-                tl = slab_entry_inflated(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, r, inv, tmin, delta);
-                goL = !(tl > prune_bound(closest));
+            float te;
+            bool g = slab(x0, y0, z0, x1, y1, z1, r, inv, T.tmin, T.tmax_entry, te);
+            if (g && T.prune) {
+                te = slab_entry_inflated(x0, y0, z0, x1, y1, z1, r, inv, T.tmin, delta);
+                g = !(te > prune_bound(T.closest));
             }
-        }
-        if (rc != rtdev::kChildEmpty) {
-            if (rc & rtdev::kLeafBit) {
-                leaf_hit_ranked(S, rc, __float_as_uint(n3.w), r, q, tmin, closest, best_rank, hit_code, any);
+            if (k) {
+                goR = g;
+                tr = te;
             } else {
-                goR = slab(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, r, inv, tmin, tmax_entry, tr);
-                if (goR && prune) {
-                    tr = slab_entry_inflated(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, r, inv, tmin, delta);
-                    goR = !(tr > prune_bound(closest));
-                }
+                goL = g;
+                tl = te;
             }
         }
-        if (goL && goR) {
-            bool left_first = tl <= tr;
-            uint32_t far = left_first ? rc : lc;
-            float tfar = left_first ? tr : tl;
-            cur = left_first ? lc : rc;
-            stk[sp * 128u] = far;
-            stk[sp * 128u + 64u] = __float_as_uint(tfar);
-            sp += 1u;
-            continue;
-        }
-        if (goL) {
-            cur = lc;
-            continue;
-        }
-        if (goR) {
-            cur = rc;
-            continue;
-        }
-        bool found = false;
-        while (sp > 0u) {
-            sp -= 1u;
-            uint32_t cand = stk[sp * 128u];
-            float tenter = __uint_as_float(stk[sp * 128u + 64u]);
-            if (!prune || !(tenter > prune_bound(closest))) {
-                cur = cand;
-                found = true;
-                break;
-            }
-        }
-        if (!found) break;
     }
-    return any;
+    PROF_ADD(kPrBvhTrip, pt);
+    if (goL && goR) {
+        bool left_first = tl <= tr;
+        uint32_t far = left_first ? rc : lc;
+        float tfar = left_first ? tr : tl;
+        T.cur = left_first ? lc : rc;
+        stk[T.sp * 128u] = far;
+        stk[T.sp * 128u + 64u] = __float_as_uint(tfar);
+        T.sp += 1u;
+        return true;
+    }
+    if (goL || goR) {
+        T.cur = goL ? lc : rc;
+        return true;
+    }
+    while (T.sp > 0u) {
+        T.sp -= 1u;
+        uint32_t cand = stk[T.sp * 128u];
+        float tenter = __uint_as_float(stk[T.sp * 128u + 64u]);
+        if (!T.prune || !(tenter > prune_bound(T.closest))) {
+            T.cur = cand;
+            return true;
+        }
+    }
+    return false;
+}
+RT_DEV bool bvh_hit(const DevScene& S, float delta, uint32_t root, const Ray& r, float tmin, float& closest,
+                    uint32_t& hit_code, uint32_t* stk, uint32_t mode) {
+    Trav T;
+    trav_init(T, S, root, root, r, tmin, closest, closest, 0u, mode);
+    while (trav_step(T, S, delta, stk)) {
+    }
+    closest = T.closest;
+    if (T.any) hit_code = T.hit_code;
+    return T.any;
 }
 
 // Translate (instance.rs:39) / RotateY (instance.rs:104-110, 121-124) applied to a ray.
@@ -520,7 +652,7 @@ RT_DEV Ray apply_op(f4 op, Ray r) {
 
 // A GEOM or BVH entry (the caller guarantees E is wave-uniform).
 RT_DEV bool entry_geom_hit(const DevScene& S, float delta, const DevEntry* E, Ray r, float tmin, float& closest,
-                           uint32_t& hit_code, uint32_t* stk, bool exact) {
+                           uint32_t& hit_code, uint32_t* stk, uint32_t exact) {
     uint32_t ntf = E->ntf;
     for (uint32_t i = 0; i < ntf; ++i) r = apply_op(E->tf[i], r);
     if (E->kind == rtdev::kEntBvh) return bvh_hit(S, delta, E->payload, r, tmin, closest, hit_code, stk, exact);
@@ -531,7 +663,7 @@ RT_DEV bool entry_geom_hit(const DevScene& S, float delta, const DevEntry* E, Ra
 // ConstantMedium::hit (hittable.rs:176-233); draws one U(0,1) once the clamped
 // interval is non-empty, exactly where the reference does.
 RT_DEV bool medium_hit(const DevScene& S, float delta, const DevEntry* E, Ray r, float tmin, float tmax, Rng& g,
-                       const Key& k, float& t_out, uint32_t* stk, bool exact) {
+                       const Key& k, float& t_out, uint32_t* stk, uint32_t exact) {
     uint32_t ntf = E->ntf;
     for (uint32_t i = 0; i < ntf; ++i) r = apply_op(E->tf[i], r);
     const DevEntry* B = S.entries + E->payload;
@@ -556,7 +688,9 @@ RT_DEV bool medium_hit(const DevScene& S, float delta, const DevEntry* E, Ray r,
     if (t1 < 0.0f) t1 = 0.0f;
     float ray_length = length(r.d);
     float distance_inside = (t2 - t1) * ray_length;
+    PROF_T0(pl);
     float hit_distance = E->neg_inv_density * rt_logf(std01(g, k));
+    PROF_ADD(kPrLog, pl);
     if (hit_distance > distance_inside) return false;
     t_out = t1 + hit_distance / ray_length;
     return true;
@@ -564,11 +698,12 @@ RT_DEV bool medium_hit(const DevScene& S, float delta, const DevEntry* E, Ray r,
 
 // HittableList::hit over the world (hittable.rs:100-118), t in [0.001, inf).
 RT_DEV bool world_hit(const DevScene& S, float delta, const Ray& r, Rng& g, const Key& k, float& t_hit,
-                      uint32_t& hit_entry, uint32_t& hit_code, uint32_t* stk, bool exact) {
+                      uint32_t& hit_entry, uint32_t& hit_code, uint32_t* stk, uint32_t exact) {
     float closest = kInf;
     bool any = false;
     for (uint32_t e = 0; e < S.num_top; ++e) {
         const DevEntry* E = S.entries + e;
+        PROF_T0(pe);
         if (E->kind == rtdev::kEntMedium) {
             float t;
             if (medium_hit(S, delta, E, r, 0.001f, closest, g, k, t, stk, exact)) {
@@ -585,6 +720,7 @@ RT_DEV bool world_hit(const DevScene& S, float delta, const Ray& r, Rng& g, cons
                 any = true;
             }
         }
+        PROF_ADD(kPrEntry0 + (e < kPrBvhTrip - kPrEntry0 - 1 ? e : kPrBvhTrip - kPrEntry0 - 1), pe);
     }
     t_hit = closest;
     return any;
@@ -763,16 +899,21 @@ RT_DEV V tex_value(const DevScene& S, uint32_t tid, float u, float v, V p) {
         uint32_t kind = T->kind;
         if (kind == rtdev::kTexSolid) return mk(T->color[0], T->color[1], T->color[2]);  // solid_color.rs:21-25
         if (kind == rtdev::kTexChecker) {                                                  // checker.rs:27-37
+            PROF_T0(pc);
             float sc = T->scale;
             float sines = rt_sinf(sc * p.x) * rt_sinf(sc * p.y) * rt_sinf(sc * p.z);
             tid = sign_negative(sines) ? T->b : T->a;
+            PROF_ADD(kPrChecker, pc);
             continue;
         }
         if (kind == rtdev::kTexMarble) {  // marble.rs:23-29
+            PROF_T0(pm);
             double n = turbulence(S.perm + 256u * T->a, (double)p.x, (double)p.y, (double)p.z);
             float s = 0.5f * (1.0f + rt_sinf(T->scale * p.z + 10.0f * (float)n));
+            PROF_ADD(kPrMarble, pm);
             return mk(s, s, s);
         }
+        PROF_T0(pi);
         // image_texture.rs:21-52
         uint32_t w = T->b, h = T->c;
         float uu = rs_clamp(u, 0.0f, 1.0f);
@@ -783,7 +924,9 @@ RT_DEV V tex_value(const DevScene& S, uint32_t tid, float u, float v, V p) {
         if (j >= h) j = h - 1u;
         const uint8_t* px = S.texels + T->a + ((size_t)j * w + i) * 3u;
         const float cs = 1.0f / 255.0f;
-        return mk((float)px[0] * cs, (float)px[1] * cs, (float)px[2] * cs);
+        V texel = mk((float)px[0] * cs, (float)px[1] * cs, (float)px[2] * cs);
+        PROF_ADD(kPrImage, pi);
+        return texel;
     }
 }
 
@@ -808,23 +951,31 @@ RT_DEV bool scatter(const DevScene& S, const DevMaterial& m, const Ray& r, const
     // Lambertian, Metal and Isotropic each draw exactly one in_unit_sphere() and
     // nothing else (lambertian.rs:36, metal.rs:30, isotropic.rs:37): draw it once here.
     V rs = mk(0.0f, 0.0f, 0.0f);
-    if (m.kind == rtdev::kMatLambertian || m.kind == rtdev::kMatMetal || m.kind == rtdev::kMatIsotropic)
+    if (m.kind == rtdev::kMatLambertian || m.kind == rtdev::kMatMetal || m.kind == rtdev::kMatIsotropic) {
+        PROF_T0(pu);
         rs = in_unit_sphere(g, k);
+        PROF_ADD(kPrUnitSphere, pu);
+    }
     if (m.kind == rtdev::kMatLambertian) {  // lambertian.rs:34-53
+        PROF_T0(pb);
         V dir = rec.n + normalize(rs);
         if (near_zero(dir)) dir = rec.n;
         sc.d = dir;
         att = tex_value(S, m.tex, rec.u, rec.v, rec.p);
+        PROF_ADD(kPrLambert, pb);
         return true;
     }
     if (m.kind == rtdev::kMatMetal) {  // metal.rs:25-43
+        PROF_T0(pt);
         V reflected = reflect(normalize(r.d), rec.n);
         V dir = reflected + m.fuzz * rs;
         sc.d = dir;
         att = mk(m.albedo[0], m.albedo[1], m.albedo[2]);
+        PROF_ADD(kPrMetal, pt);
         return dot(dir, rec.n) > 0.0f;
     }
     if (m.kind == rtdev::kMatDielectric) {  // dialectric.rs:32-61
+        PROF_T0(pd);
         att = mk(1.0f, 1.0f, 1.0f);
         float ratio = rec.front ? 1.0f / m.ior : m.ior;
         V ud = normalize(r.d);
@@ -841,11 +992,14 @@ RT_DEV bool scatter(const DevScene& S, const DevMaterial& m, const Ray& r, const
             refl = refl_p > std01(g, k);
         }
         sc.d = refl ? reflect(ud, rec.n) : refract(ud, rec.n, ratio);
+        PROF_ADD(kPrDielectric, pd);
         return true;
     }
     if (m.kind == rtdev::kMatIsotropic) {  // isotropic.rs:31-43
+        PROF_T0(ps);
         sc.d = rs;
         att = tex_value(S, m.tex, rec.u, rec.v, rec.p);
+        PROF_ADD(kPrIso, ps);
         return true;
     }
     return false;  // DiffuseLight never scatters (diffuse_light.rs:26-32)
@@ -903,7 +1057,7 @@ __global__ __launch_bounds__(64) void trace_samples(DevScene S, DevCamera C, Dev
     const uint32_t lane = threadIdx.x;
     uint32_t* stk = lds_stack + lane;  // [level][{node, t_enter}][lane]
     const Key k{P.seed_lo, P.seed_hi};
-    const bool exact = (P.flags & RT_FLAG_EXACT_BVH) != 0u;
+    const uint32_t exact = ((P.flags & RT_FLAG_EXACT_BVH) ? kModeExact : 0u) | P.tune;
     const V bg = mk(P.bg[0], P.bg[1], P.bg[2]);
 
     bool has = false;
@@ -917,9 +1071,11 @@ __global__ __launch_bounds__(64) void trace_samples(DevScene S, DevCamera C, Dev
     ray.time = 0.0f;
     uint32_t pool_batch = 0, pool_next = 0, pool_end = 0;  // wave-uniform
     bool exhausted = false;                                 // wave-uniform
+    PROF_INIT();
 
     for (;;) {
         // ---- hand items to idle lanes ------------------------------------
+        PROF_T0(pr);
         for (;;) {
             unsigned long long need = __ballot(!has);
             if (need == 0ull || exhausted) break;
@@ -961,10 +1117,12 @@ __global__ __launch_bounds__(64) void trace_samples(DevScene S, DevCamera C, Dev
             uint32_t n = (uint32_t)__popcll(need);
             pool_next += n < avail ? n : avail;
         }
+        PROF_ADD(kPrRefill, pr);
         if (__ballot(has) == 0ull) break;  // pool exhausted and every path finished
 
         // ---- one ray segment per live lane (ray.rs:32-62) -----------------
         if (has) {
+            PROF_T0(pg);
             bool done;
             if (depth == 0u) {
                 done = true;  // ray.rs:39-41
@@ -972,18 +1130,28 @@ __global__ __launch_bounds__(64) void trace_samples(DevScene S, DevCamera C, Dev
                 nseg += 1u;
                 float t;
                 uint32_t entry = 0, code = 0;
-                if (!world_hit(S, P.prune_delta, ray, g, k, t, entry, code, stk, exact)) {
+                PROF_T0(pw);
+                bool hit = world_hit(S, P.prune_delta, ray, g, k, t, entry, code, stk, exact);
+                PROF_ADD(kPrWorld, pw);
+                if (!hit) {
                     L = L + T * bg;
                     done = true;
                 } else {
                     Rec rec;
+                    PROF_T0(pc);
                     make_record(S, entry, code, t, ray, rec);
+                    PROF_ADD(kPrRecord, pc);
                     const DevMaterial m = S.mats[rec.mat];
+                    PROF_T0(pe);
                     V e = m.kind == rtdev::kMatLight ? tex_value(S, m.tex, rec.u, rec.v, rec.p) : mk(0.0f, 0.0f, 0.0f);
                     L = L + T * e;
+                    PROF_ADD(kPrEmit, pe);
                     V att;
                     Ray sc;
-                    if (scatter(S, m, ray, rec, g, k, att, sc)) {
+                    PROF_T0(ps);
+                    bool scattered = scatter(S, m, ray, rec, g, k, att, sc);
+                    PROF_ADD(kPrScatter, ps);
+                    if (scattered) {
                         T = T * att;
                         ray = sc;
                         depth -= 1u;
@@ -994,19 +1162,440 @@ __global__ __launch_bounds__(64) void trace_samples(DevScene S, DevCamera C, Dev
                 }
             }
             if (done) {
+                PROF_T0(po);
                 float* o = sbuf + ((size_t)s_local * Q.npix + pixel) * 3u;
                 o[0] = L.x;
                 o[1] = L.y;
                 o[2] = L.z;
                 has = false;
+                PROF_ADD(kPrStore, po);
             }
+            PROF_ADD(kPrSegment, pg);
         }
     }
+    PROF_FLUSH();
     if (seg_counter) {
         unsigned long long v = nseg;
         for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
         if (lane == 0u) atomicAdd(seg_counter, v);
     }
+}
+
+// ---------------------------------------------------------------------------
+// Wavefront path (scenes with top-level BVHs). The megakernel above keeps one
+// path per lane for its whole life, so a wave pays for its slowest lane inside
+// every BVH: measured 5 of 64 lanes active per traversal step on C3. Here path
+// state lives in an HBM pool (80 B per slot) and every bounce runs as
+//   wf_logic  shade the previous hit (emit / scatter), finish + regenerate,
+//             then the entries of pass 0 inline;
+//   wf_bvh    per pass: persistent traversal of the queued (slot, BVH) work,
+//             a lane takes the next ray the moment its own finishes;
+//   wf_pass   passes > 0: the next run of inline entries.
+// A pass is a run of top-level entries; its BVHs are queued, everything else is
+// tested inline. Geometry entries commute under the (t, entry, DFS rank) tie
+// rule, and a BVH's reference box tests use the t_max recorded when the inline
+// walk passed it in list order. A ConstantMedium draws its ln(U) only if its
+// clamped interval is non-empty against closest-so-far, so a pass ends before
+// any medium preceded by a queued BVH of the same pass: media always see the
+// exact list-order closest. Same draws, same candidates, same winner.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kMaxPasses = 8, kMaxPassBvh = 8;
+constexpr uint32_t kNoHit = 0xffffffffu;
+constexpr uint32_t kStFree = 0u, kStTrace = 1u;
+struct WfPass {
+    uint32_t first, last;  // inline top-level entries [first, last)
+    uint32_t nbvh;         // queued BVH entries (ascending) of this pass
+    uint32_t bvh[kMaxPassBvh];
+};
+struct WfPlan {
+    uint32_t npass;
+    WfPass pass[kMaxPasses];
+};
+// counters: two sets alternate by iteration parity (a set is zeroed by the logic
+// kernel of the previous iteration); the item counter is per chunk.
+enum : uint32_t { kCtrTrace = 0, kCtrActive = 1, kCtrQueue = 2, kCtrPull = 2 + kMaxPasses, kCtrStride = 32 };
+constexpr uint32_t kCtrItems = 2 * kCtrStride;
+struct WfPool {
+    f4* o;            // o.xyz, time
+    f4* d;            // d.xyz, closest
+    f4* tl;           // T.xyz, L.x
+    f4* lh;           // L.y, L.z, hit entry, hit code (bits)
+    uint4* m;         // pixel, chunk sample, depth | status << 16, rng block << 3 | n
+    float* tmax;      // [kMaxPassBvh][np]: t_max when the inline walk reached the BVH
+    uint32_t* trace;  // slots tracing this iteration (passes > 0 walk this list)
+    uint2* queue;     // (slot, BVH bit mask) for the current pass
+    uint32_t* ctr;
+    uint32_t np;
+};
+
+RT_DEV void rng_resume(Rng& g, uint32_t packed, uint32_t sample, uint32_t pixel, const Key& k) {
+    g.sample = sample;
+    g.pixel = pixel;
+    g.block = packed >> 3;
+    g.n = packed & 7u;
+    g.b0 = g.b1 = g.b2 = g.b3 = 0u;
+    if (g.n != 0u) {  // the cached block: recompute it, drop the 4 - n values already drawn
+        uint4 b = philox_block(g.block - 1u, sample, pixel, k.k0, k.k1);
+        if (g.n == 3u) { g.b0 = b.y; g.b1 = b.z; g.b2 = b.w; }
+        else if (g.n == 2u) { g.b0 = b.z; g.b1 = b.w; }
+        else { g.b0 = b.w; }
+    }
+}
+RT_DEV uint32_t rng_pack(const Rng& g) { return (g.block << 3) | g.n; }
+
+// Inline entries of one pass for one ray (hittable.rs:100-118 in list order).
+// Returns the mask of queued BVHs whose root box the ray enters, with their
+// list-order t_max in tmax[j * np + slot].
+RT_DEV uint32_t wf_inline(const DevScene& S, const DevParams& P, const WfPass& ps, const Ray& ray, Rng& g,
+                          const Key& k, float& closest, uint32_t& he, uint32_t& hc, float* tmax, uint32_t np,
+                          uint32_t slot, uint32_t* stk, uint32_t mode) {
+    uint32_t mask = 0u, j = 0u;
+    for (uint32_t e = ps.first; e < ps.last; ++e) {
+        const DevEntry* E = S.entries + e;
+        if (E->kind == rtdev::kEntMedium) {
+            float t;
+            if (medium_hit(S, P.prune_delta, E, ray, 0.001f, closest, g, k, t, stk, mode)) {
+                closest = t;
+                he = e;
+                hc = rtdev::leaf_code(rtdev::kLeafMedium, 0);
+            }
+        } else if (j < ps.nbvh && ps.bvh[j] == e) {
+            // the wrapper node's child box = the root box, tested like bvh.rs:370
+            Ray r = ray;
+            for (uint32_t i = 0; i < E->ntf; ++i) r = apply_op(E->tf[i], r);
+            const f4* nd = S.nodes + 4 * (size_t)E->payload;
+            f4 n0 = ld4(nd), n1 = ld4(nd + 1), n3 = ld4(nd + 3);
+            V inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
+            float te;
+            bool go = slab(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, r, inv, 0.001f, closest, te);
+            if (go && !(mode & kModeExact) && (__float_as_uint(n3.z) & rtdev::kBvhPrunable)) {
+                te = slab_entry_inflated(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, r, inv, 0.001f, P.prune_delta);
+                go = !(te > prune_bound(closest));
+            }
+            if (go) {
+                mask |= 1u << j;
+                tmax[(size_t)j * np + slot] = closest;
+            }
+            ++j;
+        } else {
+            uint32_t code;
+            if (entry_geom_hit(S, P.prune_delta, E, ray, 0.001f, closest, code, stk, mode)) {
+                he = e;
+                hc = code;
+            }
+        }
+    }
+    return mask;
+}
+
+// Wave-aggregated append of (slot, mask) to the pass queue.
+RT_DEV void wf_enqueue(const WfPool& W, uint32_t* ctr, uint32_t pass, uint32_t slot, uint32_t mask) {
+    unsigned long long b = __ballot(mask != 0u);
+    if (b == 0ull) return;
+    uint32_t lane = __lane_id();
+    uint32_t first = (uint32_t)__builtin_ctzll(b);
+    uint32_t base = 0;
+    if (lane == first) base = atomicAdd(&ctr[kCtrQueue + pass], (uint32_t)__popcll(b));
+    base = __shfl(base, (int)first);
+    if (mask != 0u) {
+        uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+        W.queue[base + rank] = make_uint2(slot, mask);
+    }
+}
+RT_DEV void wf_append_trace(const WfPool& W, uint32_t* ctr, uint32_t slot, bool on) {
+    unsigned long long b = __ballot(on);
+    if (b == 0ull) return;
+    uint32_t lane = __lane_id();
+    uint32_t first = (uint32_t)__builtin_ctzll(b);
+    uint32_t base = 0;
+    if (lane == first) base = atomicAdd(&ctr[kCtrTrace], (uint32_t)__popcll(b));
+    base = __shfl(base, (int)first);
+    if (on) {
+        uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+        W.trace[base + rank] = slot;
+    }
+}
+
+// Item -> (pixel, chunk sample): the megakernel's order (8x8 block, group of
+// kGroup samples, sample, pixel-in-block), so consecutive items are neighbours.
+RT_DEV bool wf_item(const DevParams& P, const ChunkParams& Q, uint32_t item, uint32_t& x, uint32_t& y,
+                    uint32_t& s) {
+    uint32_t batch = item / (64u * kGroup), within = item - batch * (64u * kGroup);
+    uint32_t blk_local = batch / Q.groups_per_block;
+    uint32_t grp = batch - blk_local * Q.groups_per_block;
+    s = grp * kGroup + (within >> 6);
+    uint32_t pib = within & 63u;
+    uint32_t blk = P.shard_index + blk_local * P.shard_count;
+    uint32_t by = blk / P.blocks_x, bx = blk - by * P.blocks_x;
+    x = bx * 8u + (pib & 7u);
+    y = by * 8u + (pib >> 3);
+    return x < P.width && y < P.height && s < Q.samples;
+}
+
+__global__ __launch_bounds__(64) void wf_logic(DevScene S, DevCamera C, DevParams P, ChunkParams Q, WfPool W,
+                                               const WfPlan* __restrict__ plan, uint32_t parity,
+                                               float* __restrict__ sbuf,
+                                               unsigned long long* __restrict__ seg_counter) {
+    extern __shared__ uint32_t lds_stack[];
+    const uint32_t lane = threadIdx.x;
+    uint32_t* stk = lds_stack + lane;
+    const uint32_t slot = blockIdx.x * 64u + lane;  // np is a multiple of 64
+    PROF_INIT();
+    PROF_T0(pw);
+    uint32_t* ctr = W.ctr + parity * kCtrStride;
+    if (blockIdx.x == 0u && lane < kCtrStride) W.ctr[(parity ^ 1u) * kCtrStride + lane] = 0u;
+    const Key k{P.seed_lo, P.seed_hi};
+    const uint32_t mode = ((P.flags & RT_FLAG_EXACT_BVH) ? kModeExact : 0u) | P.tune;
+
+    uint4 m = W.m[slot];
+    uint32_t status = m.z >> 16, depth = m.z & 0xffffu;
+    Rng g;
+    Ray ray;
+    V T = mk(1.0f, 1.0f, 1.0f), L = mk(0.0f, 0.0f, 0.0f);
+    bool dirty = false;
+    PROF_T0(ps);
+    if (status == kStTrace) {  // shade the segment traced last iteration (ray.rs:43-61)
+        f4 o = W.o[slot], d = W.d[slot], tl = W.tl[slot], lh = W.lh[slot];
+        ray.o = xyz(o);
+        ray.time = o.w;
+        ray.d = xyz(d);
+        T = xyz(tl);
+        L = mk(tl.w, lh.x, lh.y);
+        rng_resume(g, m.w, Q.sample0 + m.y, m.x, k);
+        uint32_t he = __float_as_uint(lh.z), hc = __float_as_uint(lh.w);
+        bool done;
+        if (he == kNoHit) {
+            L = L + T * mk(P.bg[0], P.bg[1], P.bg[2]);
+            done = true;
+        } else {
+            Rec rec;
+            make_record(S, he, hc, d.w, ray, rec);
+            const DevMaterial mt = S.mats[rec.mat];
+            V e = mt.kind == rtdev::kMatLight ? tex_value(S, mt.tex, rec.u, rec.v, rec.p) : mk(0.0f, 0.0f, 0.0f);
+            L = L + T * e;
+            V att;
+            Ray sc;
+            if (scatter(S, mt, ray, rec, g, k, att, sc)) {
+                T = T * att;
+                ray = sc;
+                depth -= 1u;
+                done = depth == 0u;
+            } else {
+                done = true;
+            }
+        }
+        if (done) {
+            float* out = sbuf + ((size_t)m.y * Q.npix + m.x) * 3u;
+            out[0] = L.x;
+            out[1] = L.y;
+            out[2] = L.z;
+            status = kStFree;
+        }
+        dirty = true;
+        PROF_ADD(kPrWfShade, ps);
+    }
+    // regenerate: idle slots take the next camera samples (renderer.rs:140-146)
+    PROF_T0(pr);
+    const uint32_t total_items = Q.num_batches * 64u * kGroup;
+    for (;;) {
+        unsigned long long need = __ballot(status == kStFree);
+        if (need == 0ull) break;
+        // once exhausted, stop adding to the counter (keeps it from wrapping)
+        if (__hip_atomic_load(&W.ctr[kCtrItems], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= total_items) break;
+        uint32_t first = (uint32_t)__builtin_ctzll(need);
+        uint32_t base = 0;
+        if (lane == first) base = atomicAdd(&W.ctr[kCtrItems], (uint32_t)__popcll(need));
+        base = __shfl(base, (int)first);
+        if (base >= total_items) break;  // items exhausted (wave-uniform)
+        if (status == kStFree) {
+            uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
+                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
+            uint32_t item = base + rank, x, y, s;
+            if (item < total_items && wf_item(P, Q, item, x, y, s)) {
+                m.x = y * P.width + x;
+                m.y = s;
+                T = mk(1.0f, 1.0f, 1.0f);
+                L = mk(0.0f, 0.0f, 0.0f);
+                start_sample(C, P, k, x, y, m.x, Q.sample0 + s, g, ray);
+                depth = P.max_depth;
+                dirty = true;
+                if (depth == 0u) {  // ray.rs:39-41: no segment, black sample
+                    float* out = sbuf + ((size_t)s * Q.npix + m.x) * 3u;
+                    out[0] = out[1] = out[2] = 0.0f;
+                } else {
+                    status = kStTrace;
+                }
+            }
+        }
+    }
+    PROF_ADD(kPrWfRegen, pr);
+    const bool trace = status == kStTrace;
+    float closest = kInf;
+    uint32_t he = kNoHit, hc = 0u, mask = 0u;
+    PROF_T0(pi);
+    if (trace) mask = wf_inline(S, P, plan->pass[0], ray, g, k, closest, he, hc, W.tmax, W.np, slot, stk, mode);
+    PROF_ADD(kPrWfInline, pi);
+    PROF_T0(pt);
+    if (dirty || trace) {
+        W.m[slot] = make_uint4(m.x, m.y, depth | (status << 16), rng_pack(g));
+        if (trace) {
+            W.o[slot] = f4{ray.o.x, ray.o.y, ray.o.z, ray.time};
+            W.d[slot] = f4{ray.d.x, ray.d.y, ray.d.z, closest};
+            W.tl[slot] = f4{T.x, T.y, T.z, L.x};
+            W.lh[slot] = f4{L.y, L.z, __uint_as_float(he), __uint_as_float(hc)};
+        }
+    }
+    if (plan->pass[0].nbvh) wf_enqueue(W, ctr, 0u, slot, mask);
+    if (plan->npass > 1u) wf_append_trace(W, ctr, slot, trace);
+    unsigned long long tb = __ballot(trace);
+    if (lane == 0u && tb) {
+        atomicAdd(&ctr[kCtrActive], (uint32_t)__popcll(tb));
+        if (seg_counter) atomicAdd(seg_counter, (unsigned long long)__popcll(tb));
+    }
+    PROF_ADD(kPrWfTail, pt);
+    PROF_ADD(kPrWfLogicWave, pw);
+    PROF_FLUSH();
+}
+
+// Passes > 0: the next run of inline entries for every tracing slot.
+__global__ __launch_bounds__(64) void wf_pass(DevScene S, DevParams P, ChunkParams Q, WfPool W,
+                                              const WfPlan* __restrict__ plan, uint32_t pass, uint32_t parity) {
+    extern __shared__ uint32_t lds_stack[];
+    const uint32_t lane = threadIdx.x;
+    uint32_t* stk = lds_stack + lane;
+    uint32_t* ctr = W.ctr + parity * kCtrStride;
+    const uint32_t n = ctr[kCtrTrace];
+    const Key k{P.seed_lo, P.seed_hi};
+    const uint32_t mode = ((P.flags & RT_FLAG_EXACT_BVH) ? kModeExact : 0u) | P.tune;
+    const WfPass& ps = plan->pass[pass];
+    PROF_INIT();
+    PROF_T0(pw);
+    for (uint32_t i0 = blockIdx.x * 64u; i0 < n; i0 += gridDim.x * 64u) {
+        uint32_t i = i0 + lane;
+        bool on = i < n;
+        uint32_t slot = on ? W.trace[i] : 0u, mask = 0u;
+        if (on) {
+            f4 o = W.o[slot], d = W.d[slot], lh = W.lh[slot];
+            uint4 m = W.m[slot];
+            Ray ray;
+            ray.o = xyz(o);
+            ray.time = o.w;
+            ray.d = xyz(d);
+            Rng g;
+            rng_resume(g, m.w, Q.sample0 + m.y, m.x, k);
+            float closest = d.w;
+            uint32_t he = __float_as_uint(lh.z), hc = __float_as_uint(lh.w);
+            uint32_t n0 = g.block * 8u + g.n;
+            mask = wf_inline(S, P, ps, ray, g, k, closest, he, hc, W.tmax, W.np, slot, stk, mode);
+            if (closest != d.w || he != __float_as_uint(lh.z) || hc != __float_as_uint(lh.w)) {
+                W.d[slot].w = closest;
+                W.lh[slot] = f4{lh.x, lh.y, __uint_as_float(he), __uint_as_float(hc)};
+            }
+            if (g.block * 8u + g.n != n0) W.m[slot].w = rng_pack(g);
+        }
+        if (ps.nbvh) wf_enqueue(W, ctr, pass, slot, on ? mask : 0u);
+    }
+    PROF_ADD(kPrWfPassWave, pw);
+    PROF_FLUSH();
+}
+
+// Set up the traversal of the lowest BVH bit of `mask` for `slot`; returns its entry.
+RT_DEV uint32_t wf_job_start(Trav& T, const DevScene& S, const WfPool& W, const WfPass& ps, uint32_t slot,
+                             uint32_t mask, float closest, uint32_t he, uint32_t mode) {
+    uint32_t j = (uint32_t)__builtin_ctz(mask);
+    uint32_t e = ps.bvh[j];
+    const DevEntry* E = S.entries + e;
+    f4 o = W.o[slot], d = W.d[slot];
+    Ray r;
+    r.o = xyz(o);
+    r.time = o.w;
+    r.d = xyz(d);
+    for (uint32_t i = 0; i < E->ntf; ++i) r = apply_op(E->tf[i], r);
+    uint32_t wrapper = E->payload;
+    uint32_t root = __float_as_uint(S.nodes[4 * (size_t)wrapper + 3].x);
+    uint32_t best_rank = (he != kNoHit && he > e) ? 0xffffffffu : 0u;
+    trav_init(T, S, wrapper, root, r, 0.001f, W.tmax[(size_t)j * W.np + slot], closest, best_rank, mode);
+    return e;
+}
+
+// Persistent traversal of the pass queue: each lane owns one (slot, BVH) job at a
+// time and takes the next job as soon as its traversal ends, so lanes do not
+// wait for the slowest ray of their wave.
+__global__ __launch_bounds__(64, 5) void wf_bvh(DevScene S, DevParams P, WfPool W, const WfPlan* __restrict__ plan,
+                                             uint32_t pass, uint32_t parity) {
+    extern __shared__ uint32_t lds_stack[];
+    const uint32_t lane = threadIdx.x;
+    uint32_t* stk = lds_stack + lane;
+    uint32_t* ctr = W.ctr + parity * kCtrStride;
+    const uint32_t qn = ctr[kCtrQueue + pass];
+    const uint32_t mode = ((P.flags & RT_FLAG_EXACT_BVH) ? kModeExact : 0u) | P.tune;
+    const WfPass& ps = plan->pass[pass];
+
+    bool has = false;
+    uint32_t slot = 0, mask = 0, e = 0, he = kNoHit, hc = 0, he0 = kNoHit;
+    float closest0 = kInf;
+    Trav T;
+    uint32_t pool_next = 0, pool_end = 0;  // wave-uniform: this wave's share of the queue
+    bool exhausted = false;
+    PROF_INIT();
+    PROF_T0(pw);
+
+
+    for (;;) {
+        unsigned long long need = __ballot(!has);
+        PROF_T0(pf);
+        while (need != 0ull && !exhausted) {
+            if (pool_next == pool_end) {
+                uint32_t b = 0;
+                if (lane == 0u) b = atomicAdd(&ctr[kCtrPull + pass], 64u);
+                b = __builtin_amdgcn_readfirstlane(b);
+                if (b >= qn) {
+                    exhausted = true;
+                    break;
+                }
+                pool_next = b;
+                pool_end = b + 64u < qn ? b + 64u : qn;
+            }
+            uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
+                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
+            uint32_t avail = pool_end - pool_next;
+            if (!has && rank < avail) {
+                uint2 q = W.queue[pool_next + rank];
+                slot = q.x;
+                mask = q.y;
+                f4 lh = W.lh[slot];
+                he0 = he = __float_as_uint(lh.z);
+                hc = __float_as_uint(lh.w);
+                closest0 = W.d[slot].w;
+                e = wf_job_start(T, S, W, ps, slot, mask, closest0, he, mode);
+                has = true;
+            }
+            uint32_t taken = (uint32_t)__popcll(need);
+            pool_next += taken < avail ? taken : avail;
+            need = __ballot(!has);
+        }
+        PROF_ADD(kPrWfBvhRefill, pf);
+        if (__ballot(has) == 0ull) break;
+        if (has && !trav_step(T, S, P.prune_delta, stk)) {
+            if (T.any) {
+                he = e;
+                hc = T.hit_code;
+            }
+            mask &= mask - 1u;
+            if (mask != 0u) {
+                e = wf_job_start(T, S, W, ps, slot, mask, T.closest, he, mode);  // closest carries over
+            } else {
+                if (he != he0 || T.closest != closest0 || T.any) {
+                    W.d[slot].w = T.closest;
+                    f4 lh = W.lh[slot];
+                    W.lh[slot] = f4{lh.x, lh.y, __uint_as_float(he), __uint_as_float(hc)};
+                }
+                has = false;
+            }
+        }
+    }
+    PROF_ADD(kPrWfBvhWave, pw);
+    PROF_FLUSH();
 }
 
 // color_accumulator += ray_color(...) in sample order, then / spp (renderer.rs:140-147).
@@ -1075,6 +1664,17 @@ struct rt_scene {
     hipEvent_t ev[kEvents][2] = {};
     int ev_count = 0;
     bool ev_overflow = false;
+    // wavefront path (scenes with top-level BVHs): plan, path pool, round sync
+    WfPlan plan{};
+    WfPlan* d_plan = nullptr;  // device copy (kernels index it dynamically)
+    bool wf = false;
+    uint32_t max_pass_bvh = 0;
+    void* wf_mem = nullptr;
+    uint32_t wf_np = 0;  // slots the pool was allocated for
+    WfPool wp{};
+    uint32_t* h_active = nullptr;  // pinned, one per round parity
+    hipEvent_t round_ev[2] = {};
+    int grid_pass = 0, grid_bvh = 0;
 };
 
 namespace {
@@ -1132,6 +1732,144 @@ int rt_device_count(int* count) {
     *count = n;
     return RT_OK;
 }
+
+namespace {
+
+// Split the top-level list into passes (see the wavefront notes above): every
+// top-level BVH is queued; a pass ends before a medium that follows a queued
+// BVH of the same pass, or when a pass holds kMaxPassBvh BVHs.
+bool build_plan(const rthost::HostScene& hs, WfPlan* plan, uint32_t* max_bvh) {
+    memset(plan, 0, sizeof *plan);
+    *max_bvh = 0;
+    WfPass cur{};
+    uint32_t n = 0, nbvh_total = 0;
+    auto close = [&](uint32_t last) {
+        cur.last = last;
+        if (n < kMaxPasses) plan->pass[n] = cur;
+        ++n;
+        if (cur.nbvh > *max_bvh) *max_bvh = cur.nbvh;
+        cur = WfPass{};
+        cur.first = last;
+    };
+    for (uint32_t e = 0; e < hs.num_top; ++e) {
+        uint32_t kind = hs.entries[e].kind;
+        if ((kind == rtdev::kEntMedium && cur.nbvh > 0) || (kind == rtdev::kEntBvh && cur.nbvh == kMaxPassBvh))
+            close(e);
+        if (kind == rtdev::kEntBvh) {
+            cur.bvh[cur.nbvh++] = e;
+            ++nbvh_total;
+        }
+    }
+    close(hs.num_top);
+    plan->npass = n;
+    return n <= kMaxPasses && nbvh_total > 0;
+}
+
+int wf_alloc(rt_scene* s, uint32_t np) {
+    if (s->wf_np >= np && s->wf_mem) return RT_OK;
+    if (s->wf_mem) (void)hipFree(s->wf_mem);
+    s->wf_mem = nullptr;
+    s->wf_np = 0;
+    const uint64_t nb = s->max_pass_bvh ? s->max_pass_bvh : 1u;
+    const uint64_t sizes[] = {16ull * np, 16ull * np, 16ull * np, 16ull * np, 16ull * np, 4ull * nb * np,
+                              4ull * np, 8ull * np, 512, sizeof(WfPlan)};
+    uint64_t off[10], total = 0;
+    for (int i = 0; i < 10; ++i) {
+        off[i] = total;
+        total += (sizes[i] + 255u) & ~255ull;
+    }
+    hipError_t e = hipMalloc(&s->wf_mem, total);
+    if (e != hipSuccess) {
+        s->wf_mem = nullptr;
+        return rthost::set_error(RT_ERR_OOM, std::string("hipMalloc path pool: ") + hipGetErrorString(e));
+    }
+    uint8_t* b = (uint8_t*)s->wf_mem;
+    WfPool& W = s->wp;
+    W.o = (f4*)(b + off[0]);
+    W.d = (f4*)(b + off[1]);
+    W.tl = (f4*)(b + off[2]);
+    W.lh = (f4*)(b + off[3]);
+    W.m = (uint4*)(b + off[4]);
+    W.tmax = (float*)(b + off[5]);
+    W.trace = (uint32_t*)(b + off[6]);
+    W.queue = (uint2*)(b + off[7]);
+    W.ctr = (uint32_t*)(b + off[8]);
+    W.np = np;
+    s->wf_np = np;
+    s->d_plan = (WfPlan*)(b + off[9]);
+    if ((e = hipMemcpy(s->d_plan, &s->plan, sizeof(WfPlan), hipMemcpyHostToDevice)) != hipSuccess)
+        return hip_fail(e, "upload pass plan");
+    if (!s->h_active && hipHostMalloc((void**)&s->h_active, 2 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess) {
+        s->h_active = nullptr;
+        return rthost::set_error(RT_ERR_OOM, "hipHostMalloc");
+    }
+    for (int i = 0; i < 2; ++i)
+        if (!s->round_ev[i] && (e = hipEventCreateWithFlags(&s->round_ev[i], hipEventDisableTiming)) != hipSuccess)
+            return hip_fail(e, "hipEventCreate");
+    return RT_OK;
+}
+
+// One chunk's trace stage on the wavefront path. Rounds of kRound iterations are
+// queued back to back; the host waits for round r-1's active count while round r
+// runs, and stops once a logic pass found no live path (items exhausted).
+int wf_trace(rt_scene* s, const DevCamera& cam, const DevParams& dp, const ChunkParams& q, size_t lds,
+             unsigned long long* d_segments, hipStream_t st) {
+    uint64_t total_items = (uint64_t)q.num_batches * 64u * kGroup;
+    uint32_t np_max = 4u << 20;
+    if (const char* env = getenv("RT_WF_POOL")) np_max = (uint32_t)strtoul(env, nullptr, 10);
+    if (np_max < 64u) np_max = 64u;
+    uint64_t np64 = total_items < np_max ? total_items : np_max;
+    uint32_t np = (uint32_t)((np64 + 63u) & ~63ull);
+    int rc = wf_alloc(s, np);
+    if (rc) return rc;
+    WfPool W = s->wp;
+    W.np = np;
+    hipError_t e;
+    if ((e = hipMemsetAsync(W.ctr, 0, 512, st)) != hipSuccess) return hip_fail(e, "memset counters");
+    if ((e = hipMemsetAsync(W.m, 0, 16ull * np, st)) != hipSuccess) return hip_fail(e, "memset pool");
+    if (s->grid_pass == 0) {
+        int cus = 0, a = 0, b = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s->device) != hipSuccess || cus < 1)
+            cus = 256;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, wf_pass, 64, lds) != hipSuccess || a < 1) a = 8;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, wf_bvh, 64, lds) != hipSuccess || b < 1) b = 8;
+        s->grid_pass = a * cus;
+        s->grid_bvh = b * cus;
+    }
+    const uint32_t kRound = 32;
+    const uint64_t max_iters = 64ull + (uint64_t)(dp.max_depth + 1u) * (total_items + np - 1u) / np * 64u;
+    uint64_t it = 0;
+    for (uint32_t round = 0;; ++round) {
+        for (uint32_t i = 0; i < kRound; ++i, ++it) {
+            uint32_t parity = (uint32_t)(it & 1u);
+            hipLaunchKernelGGL(wf_logic, dim3(np / 64u), dim3(64), lds, st, s->dev, cam, dp, q, W, s->d_plan, parity,
+                               s->sbuf, d_segments);
+            for (uint32_t p = 0; p < s->plan.npass; ++p) {
+                if (p > 0)
+                    hipLaunchKernelGGL(wf_pass, dim3((uint32_t)s->grid_pass), dim3(64), lds, st, s->dev, dp, q, W,
+                                       s->d_plan, p, parity);
+                if (s->plan.pass[p].nbvh)
+                    hipLaunchKernelGGL(wf_bvh, dim3((uint32_t)s->grid_bvh), dim3(64), lds, st, s->dev, dp, W, s->d_plan,
+                                       p, parity);
+            }
+        }
+        if ((e = hipGetLastError()) != hipSuccess) return hip_fail(e, "wavefront launch");
+        uint32_t last = (uint32_t)((it - 1u) & 1u);
+        if ((e = hipMemcpyAsync(&s->h_active[round & 1u], W.ctr + last * kCtrStride + kCtrActive, sizeof(uint32_t),
+                                hipMemcpyDeviceToHost, st)) != hipSuccess)
+            return hip_fail(e, "active count");
+        if ((e = hipEventRecord(s->round_ev[round & 1u], st)) != hipSuccess) return hip_fail(e, "round event");
+        if (round > 0) {
+            if ((e = hipEventSynchronize(s->round_ev[(round - 1u) & 1u])) != hipSuccess) return hip_fail(e, "round sync");
+            if (s->h_active[(round - 1u) & 1u] == 0u) break;
+        }
+        if (it > max_iters)
+            return rthost::set_error(RT_ERR_HIP, "wavefront trace did not drain (" + std::to_string(it) + " iterations)");
+    }
+    return RT_OK;
+}
+
+}  // namespace
 
 int rt_scene_upload(const rt_scene_desc* desc, int device, rt_scene_handle* out) {
     rthost::clear_error();
@@ -1205,6 +1943,7 @@ int rt_scene_upload(const rt_scene_desc* desc, int device, rt_scene_handle* out)
     d.num_entries = (uint32_t)hs.entries.size();
     d.stack_depth = hs.max_bvh_depth + 1u;
     s->coord_bound = hs.coord_bound;
+    s->wf = build_plan(hs, &s->plan, &s->max_pass_bvh);
     uint64_t c[10] = {hs.entries.size(), hs.sph.size(), hs.msph.size() / 3, hs.rect.size() / 2, hs.tri.size() / 3,
                       hs.nodes.size() / 2, hs.mats.size(), hs.texs.size(), hs.max_bvh_depth, total};
     memcpy(s->counts, c, sizeof c);
@@ -1217,7 +1956,22 @@ int rt_scene_free(rt_scene_handle s) {
     if (!s) return RT_OK;
     {
         DeviceGuard g(s->device);
+#ifdef RT_PROFILE_REGIONS
+        static unsigned long long hc[kProfCopies * 3 * kPrCount];
+        unsigned long long h[3 * kPrCount] = {};
+        if (hipDeviceSynchronize() == hipSuccess && hipMemcpyFromSymbol(hc, HIP_SYMBOL(g_prof), sizeof hc) == hipSuccess) {
+            for (uint32_t c = 0; c < kProfCopies; ++c)
+                for (uint32_t i = 0; i < 3u * kPrCount; ++i) h[i] += hc[c * 3u * kPrCount + i];
+            fprintf(stderr, "{\"rt_profile\": [");
+            for (uint32_t i = 0; i < 3u * kPrCount; ++i) fprintf(stderr, "%s%llu", i ? "," : "", h[i]);
+            fprintf(stderr, "]}\n");
+        }
+#endif
         if (s->pool) (void)hipFree(s->pool);
+        if (s->wf_mem) (void)hipFree(s->wf_mem);
+        if (s->h_active) (void)hipHostFree(s->h_active);
+        for (int i = 0; i < 2; ++i)
+            if (s->round_ev[i]) (void)hipEventDestroy(s->round_ev[i]);
         if (s->sbuf) (void)hipFree(s->sbuf);
         if (s->counter) (void)hipFree(s->counter);
         for (int i = 0; i < rt_scene::kEvents; ++i)
@@ -1258,6 +2012,10 @@ int rt_render_launch(rt_scene_handle s, const rt_camera_desc* camera, const rt_r
     dp.blocks_x = (p->width + 7u) / 8u;
     dp.num_blocks = dp.blocks_x * ((p->height + 7u) / 8u);
     dp.flags = p->flags;
+    {
+        const char* tune = getenv("RT_TUNE");  // diagnostic traversal switches (kMode* bits), default 0
+        dp.tune = tune ? (uint32_t)strtoul(tune, nullptr, 0) & ~kModeExact : 0u;
+    }
     dp.bg[0] = p->background[0];
     dp.bg[1] = p->background[1];
     dp.bg[2] = p->background[2];
@@ -1327,9 +2085,13 @@ int rt_render_launch(rt_scene_handle s, const rt_camera_desc* camera, const rt_r
             s->ev_overflow = true;
         }
         if (evp) (void)hipEventRecord(evp[0], st);
-        hipLaunchKernelGGL(trace_samples, dim3(grid), dim3(64), lds, st, s->dev, cam, dp, q, s->sbuf, s->counter,
-                           d_segments);
-        if ((e = hipGetLastError()) != hipSuccess) return hip_fail(e, "trace_samples launch");
+        if (s->wf && (dp.tune & kModeWavefront)) {
+            if ((rc = wf_trace(s, cam, dp, q, lds, d_segments, st))) return rc;
+        } else {
+            hipLaunchKernelGGL(trace_samples, dim3(grid), dim3(64), lds, st, s->dev, cam, dp, q, s->sbuf, s->counter,
+                               d_segments);
+            if ((e = hipGetLastError()) != hipSuccess) return hip_fail(e, "trace_samples launch");
+        }
         if (evp) {
             (void)hipEventRecord(evp[1], st);
             s->ev_count++;

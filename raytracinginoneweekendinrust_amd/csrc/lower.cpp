@@ -495,6 +495,7 @@ class Lowerer {
         uint32_t child[2];  // temp node index or leaf code
         bool is_node[2];
         Box box;
+        Box leaf_box[2];    // box of a leaf child (device-side conservative leaf test)
     };
 
     int bvh_build(const rt_node& n, uint32_t* root_out) {
@@ -530,18 +531,22 @@ class Lowerer {
             if (depth > max_depth_) max_depth_ = depth;
             int axis = ax.axis();
             TNode t;
+            t.leaf_box[0] = t.leaf_box[1] = Box{{0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f}};
             if (cnt == 1) {
                 t.child[0] = o[0].code;
                 t.is_node[0] = false;
                 t.child[1] = rtdev::kChildEmpty;  // same object twice in the reference: tested once here
                 t.is_node[1] = false;
                 t.box = box_union(o[0].box01, o[0].box01);
+                t.leaf_box[0] = o[0].box01;
             } else if (cnt == 2) {
                 int a = total_cmp(o[0].key[axis], o[1].key[axis]) < 0 ? 0 : 1;
                 t.child[0] = o[a].code;
                 t.child[1] = o[1 - a].code;
                 t.is_node[0] = t.is_node[1] = false;
                 t.box = box_union(o[a].box01, o[1 - a].box01);
+                t.leaf_box[0] = o[a].box01;
+                t.leaf_box[1] = o[1 - a].box01;
             } else {
                 std::stable_sort(o, o + cnt, [axis](const LeafInfo& p, const LeafInfo& q) {
                     return total_cmp(p.key[axis], q.key[axis]) < 0;
@@ -600,7 +605,7 @@ class Lowerer {
                     cb[k] = tn[tn[i].child[k]].box;
                     cc[k] = remap[tn[i].child[k]];
                 } else {
-                    cb[k] = none;
+                    cb[k] = tn[i].child[k] == rtdev::kChildEmpty ? none : tn[i].leaf_box[k];
                     cc[k] = tn[i].child[k];
                 }
             }

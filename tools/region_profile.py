@@ -1,0 +1,83 @@
+#!/usr/bin/env python3
+"""Per-region wave-cycle profile of trace_samples (diagnostic, GPU box only).
+
+    RT_LIBRARY=raytracinginoneweekendinrust_amd/_lib/librtamd_prof.so \
+        python3 tools/region_profile.py [--config C3] [--spp 64]
+
+Renders one frame with the region-instrumented build and prints, per region,
+the share of wave cycles, wave executions and the mean active lanes when the
+region ran (64 = fully converged). Regions nest: Segment contains World, Record,
+Emit, Scatter and Store; World contains the per-entry rows; Scatter contains the
+material rows; materials contain the texture rows.
+"""
+import argparse
+import json
+import os
+import sys
+import tempfile
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+NAMES = ["Refill", "Segment", "World", "Record", "Emit", "Scatter", "Marble", "Store", "Checker", "Image",
+         "UnitSphere", "Dielectric", "Lambert", "Metal", "Isotropic", "MediumLog"]
+COUNT = 48
+EXTRA = {32: "wf_logic: shade", 33: "wf_logic: regenerate", 34: "wf_logic: inline pass 0",
+         35: "wf_logic: enqueue + counters", 36: "wf_logic: whole wave", 37: "wf_pass: whole wave",
+         38: "wf_bvh: job start", 39: "wf_bvh: refill", 40: "wf_bvh: whole wave", 41: "wf: state load",
+         44: "BVH loop trip", 45: "BVH leaf test"}
+ENTRY0 = 16
+SHOWCASE = ["boxes BVH", "light rect", "moving sphere", "glass sphere", "metal sphere", "medium boundary",
+            "blue medium", "fog medium", "earth", "marble", "spheres BVH (RotY+Tr)"]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="C3")
+    ap.add_argument("--spp", type=int, default=None)
+    args = ap.parse_args()
+    if "prof" not in os.environ.get("RT_LIBRARY", ""):
+        sys.exit("set RT_LIBRARY to the _prof build")
+    import torch
+    import raytracinginoneweekendinrust_amd as rt
+    cfg = rt.CONFIGS[args.config]
+    if args.spp:
+        cfg = cfg.scaled(cfg.width, args.spp)
+    scene = rt.Scene.generate(cfg.scene, cfg.scene_seed)
+    ds = rt.DeviceScene(scene)
+    p = rt.render_params(cfg.width, cfg.height, cfg.spp, cfg.depth, background=cfg.background(), seed=cfg.render_seed)
+    out = torch.zeros(cfg.width * cfg.height * 3, dtype=torch.float32, device="cuda")
+    seg = torch.zeros(1, dtype=torch.int64, device="cuda")
+    ds.launch(cfg.camera(), p, out.data_ptr(), seg.data_ptr(), 0)
+    torch.cuda.synchronize()
+    ms, n = ds.trace_time(reset=True)
+    segments = int(seg.item())
+    # the library prints its counters on stderr when the scene is freed
+    sys.stderr.flush()
+    saved = os.dup(2)
+    with tempfile.TemporaryFile(mode="w+") as tf:
+        os.dup2(tf.fileno(), 2)
+        ds.close()
+        os.dup2(saved, 2)
+        tf.seek(0)
+        lines = [ln for ln in tf.read().splitlines() if ln.startswith('{"rt_profile"')]
+    v = json.loads(lines[-1])["rt_profile"]
+    cyc, cnt, lanes = v[:COUNT], v[COUNT:2 * COUNT], v[2 * COUNT:]
+    total = (cyc[0] + cyc[1]) or (cyc[36] + cyc[37] + cyc[40])
+    samples = cfg.width * cfg.height * cfg.spp
+    print(f"{cfg.name} {cfg.width}x{cfg.height} {cfg.spp}spp: trace {ms:.1f} ms, {segments} segments, "
+          f"{segments / samples:.3f} seg/sample, wave cycles refill+segment = {total:.4g}")
+    rows = []
+    for i in range(COUNT):
+        if cnt[i] == 0:
+            continue
+        name = EXTRA[i] if i in EXTRA else NAMES[i] if i < ENTRY0 else (f"entry {i - ENTRY0}: " + (SHOWCASE[i - ENTRY0] if cfg.scene == "showcase"
+                                                                        and i - ENTRY0 < len(SHOWCASE) else ""))
+        rows.append((name, cyc[i] / total, cnt[i], lanes[i] / cnt[i], cyc[i] / cnt[i]))
+    print(f"{'region':34s} {'cyc%':>7s} {'wave-execs':>12s} {'lanes':>6s} {'cyc/exec':>9s}")
+    for name, frac, c, ln, ce in rows:
+        print(f"{name:34s} {100 * frac:7.2f} {c:12d} {ln:6.1f} {ce:9.0f}")
+
+
+if __name__ == "__main__":
+    main()
