@@ -58,12 +58,11 @@ constexpr float kInf = __builtin_inff();
 enum ProfRegion : uint32_t {
     kPrRefill = 0, kPrSegment, kPrWorld, kPrRecord, kPrEmit, kPrScatter, kPrMarble, kPrStore,
     kPrChecker, kPrImage, kPrUnitSphere, kPrDielectric, kPrLambert, kPrMetal, kPrIso, kPrLog,
-    kPrEntry0 = 16, kPrWfShade = 32, kPrWfRegen, kPrWfInline, kPrWfTail, kPrWfLogicWave, kPrWfPassWave,
-    kPrWfBvhStart, kPrWfBvhRefill, kPrWfBvhWave, kPrWfLoad, kPrBvhTrip = 44, kPrLeafTest = 45, kPrCount = 48
+    kPrEntry0 = 16, kPrEntryLast = 43, kPrBvhTrip = 44, kPrLeafTest = 45, kPrCount = 48
 };
 // traversal mode bits (bvh_hit): kModeExact = RT_FLAG_EXACT_BVH; the rest come
 // from DevParams::tune (RT_TUNE environment variable, diagnostics / A-B runs).
-constexpr uint32_t kModeExact = 1u, kModeNoLeafBoxes = 2u, kModeWavefront = 4u;
+constexpr uint32_t kModeExact = 1u, kModeNoLeafBoxes = 2u;
 #ifdef RT_PROFILE_REGIONS
 constexpr uint32_t kProfCopies = 64;  // flush targets spread over blockIdx to keep atomics uncontended
 __device__ unsigned long long g_prof[kProfCopies * 3 * kPrCount];
@@ -89,6 +88,15 @@ __device__ __forceinline__ void prof_add(uint32_t region, uint64_t t0) {
 }
 #define PROF_INIT() prof_init()
 #define PROF_FLUSH() prof_flush()
+// Leaf-box audit (profiling build): leaves rejected by leaf_box_may_hit are
+// tested anyway; a rejected leaf that would have won is recorded here.
+struct LeafAudit {
+    float o[3], d[3], tmin, closest, t, box[6], delta;
+    uint32_t code, rank, best_rank;
+};
+constexpr uint32_t kAuditMax = 64;
+__device__ unsigned g_audit_count;
+__device__ LeafAudit g_audit[kAuditMax];
 #else
 #define PROF_T0(name) do { } while (0)
 #define PROF_ADD(region, t0) do { } while (0)
@@ -522,120 +530,120 @@ RT_DEV bool leaf_box_may_hit(float x0, float y0, float z0, float x1, float y1, f
 // t_max the BVH was entered with), so no node outside the reference's visit set
 // is ever entered. For BVHs flagged kBvhPrunable (f64 spheres / rects / cubes)
 // a visited subtree is additionally skipped when its entry into the box
-// inflated by P.prune_delta lies beyond prune_bound(closest): such a subtree
-// provably holds no candidate that could beat (closest, rank). Children are
-// visited nearest-first; ties resolve by DFS rank exactly like the recursion.
+// inflated by P.prune_delta lies beyond prune_bound(closest), and a leaf is
+// skipped when its own inflated box rules out a hit in [tmin, closest]: such
+// candidates provably cannot beat (closest, rank). Children are visited
+// nearest-first; ties resolve by DFS rank exactly like the recursion.
 // The stack lives in LDS, lane-strided: stack[level * 128 + {0, 64} + lane].
-//
-// The traversal is a resumable state machine (trav_init / trav_step, one node
-// per step) so the wavefront BVH kernel can interleave many rays per lane.
-struct Trav {
-    Ray r;
-    V inv;
-    RayD q;
-    float tmin, tmax_entry, closest;
-    uint32_t best_rank, hit_code, sp, cur;
-    bool any, prune, leaf_boxes;
-};
-// closest / best_rank: the candidate to beat; best_rank = 0 lets an equal-t leaf
-// win (the BVH comes later in list order), ~0u makes it lose.
-// wrapper = the BVH's wrapper node (holds the prunable flag); start = first node
-// to visit (the wrapper itself, or its child once the root box test passed).
-RT_DEV void trav_init(Trav& T, const DevScene& S, uint32_t wrapper, uint32_t start, const Ray& r, float tmin,
-                      float tmax_entry, float closest, uint32_t best_rank, uint32_t mode) {
-    T.r = r;
-    T.inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
-    T.q = to_d(r);
-    T.tmin = tmin;
-    T.tmax_entry = tmax_entry;
-    T.closest = closest;
-    T.best_rank = best_rank;
-    T.hit_code = 0u;
-    T.sp = 0u;
-    T.cur = start;
-    T.any = false;
-    T.prune = !(mode & kModeExact) && (__float_as_uint(S.nodes[4 * (size_t)wrapper + 3].z) & rtdev::kBvhPrunable) != 0u;
-    T.leaf_boxes = T.prune && !(mode & kModeNoLeafBoxes);
-}
-// Visits node T.cur; returns false once the traversal is complete. The two
-// children go through one loop (not unrolled) so the leaf tests exist once in
-// the code: inlining them per child doubled the kernel's register footprint.
-RT_DEV bool trav_step(Trav& T, const DevScene& S, float delta, uint32_t* stk) {
-    // by-value copies: a select between struct members (rect_axes) would
-    // otherwise become a select of addresses and pin T in scratch memory
-    const Ray r = T.r;
-    const V inv = T.inv;
-    const RayD q = T.q;
-    const f4* nd = S.nodes + 4 * (size_t)T.cur;
-    f4 n0 = ld4(nd), n1 = ld4(nd + 1), n2 = ld4(nd + 2), n3 = ld4(nd + 3);
-    const uint32_t lc = __float_as_uint(n3.x), rc = __float_as_uint(n3.y);
-    bool goL = false, goR = false;
-    float tl = 0.0f, tr = 0.0f;
-    PROF_T0(pt);
-#pragma unroll 1
-    for (uint32_t k = 0; k < 2u; ++k) {
-        const uint32_t c = k ? rc : lc;
-        if (c == rtdev::kChildEmpty) continue;
-        float x0 = k ? n1.z : n0.x, y0 = k ? n1.w : n0.y, z0 = k ? n2.x : n0.z;
-        float x1 = k ? n2.y : n0.w, y1 = k ? n2.z : n1.x, z1 = k ? n2.w : n1.y;
-        if (c & rtdev::kLeafBit) {
-            if (!T.leaf_boxes || leaf_box_may_hit(x0, y0, z0, x1, y1, z1, r, inv, T.tmin, T.closest, delta)) {
-                PROF_T0(pl);
-                leaf_hit_ranked(S, c, __float_as_uint(k ? n3.w : n3.z), r, q, T.tmin, T.closest, T.best_rank,
-                                T.hit_code, T.any);
-                PROF_ADD(kPrLeafTest, pl);
-            }
-        } else {
-            float te;
-            bool g = slab(x0, y0, z0, x1, y1, z1, r, inv, T.tmin, T.tmax_entry, te);
-            if (g && T.prune) {
-                te = slab_entry_inflated(x0, y0, z0, x1, y1, z1, r, inv, T.tmin, delta);
-                g = !(te > prune_bound(T.closest));
-            }
-            if (k) {
-                goR = g;
-                tr = te;
-            } else {
-                goL = g;
-                tl = te;
-            }
-        }
-    }
-    PROF_ADD(kPrBvhTrip, pt);
-    if (goL && goR) {
-        bool left_first = tl <= tr;
-        uint32_t far = left_first ? rc : lc;
-        float tfar = left_first ? tr : tl;
-        T.cur = left_first ? lc : rc;
-        stk[T.sp * 128u] = far;
-        stk[T.sp * 128u + 64u] = __float_as_uint(tfar);
-        T.sp += 1u;
-        return true;
-    }
-    if (goL || goR) {
-        T.cur = goL ? lc : rc;
-        return true;
-    }
-    while (T.sp > 0u) {
-        T.sp -= 1u;
-        uint32_t cand = stk[T.sp * 128u];
-        float tenter = __uint_as_float(stk[T.sp * 128u + 64u]);
-        if (!T.prune || !(tenter > prune_bound(T.closest))) {
-            T.cur = cand;
-            return true;
-        }
-    }
-    return false;
-}
+#ifdef RT_PROFILE_REGIONS
+// Leaf-box audit (profiling build): a leaf rejected by leaf_box_may_hit is tested
+// anyway, and recorded if it would have produced a candidate.
+#define LEAF_AUDIT(CODE_, RANK_, X0_, Y0_, Z0_, X1_, Y1_, Z1_)                                          \
+    do {                                                                                               \
+        float c_ = closest;                                                                            \
+        uint32_t br_ = best_rank, hc_ = 0u;                                                            \
+        bool any_ = false;                                                                             \
+        leaf_hit_ranked(S, (CODE_), (RANK_), r, q, tmin, c_, br_, hc_, any_);                          \
+        if (any_) {                                                                                    \
+            unsigned i_ = atomicAdd(&g_audit_count, 1u);                                               \
+            if (i_ < kAuditMax) {                                                                      \
+                LeafAudit& A = g_audit[i_];                                                            \
+                A.o[0] = r.o.x; A.o[1] = r.o.y; A.o[2] = r.o.z;                                        \
+                A.d[0] = r.d.x; A.d[1] = r.d.y; A.d[2] = r.d.z;                                        \
+                A.tmin = tmin; A.closest = closest; A.t = c_; A.delta = delta;                         \
+                A.box[0] = (X0_); A.box[1] = (Y0_); A.box[2] = (Z0_);                                  \
+                A.box[3] = (X1_); A.box[4] = (Y1_); A.box[5] = (Z1_);                                  \
+                A.code = (CODE_); A.rank = (RANK_); A.best_rank = best_rank;                           \
+            }                                                                                          \
+        }                                                                                              \
+    } while (0)
+#else
+#define LEAF_AUDIT(CODE_, RANK_, X0_, Y0_, Z0_, X1_, Y1_, Z1_) do { } while (0)
+#endif
 RT_DEV bool bvh_hit(const DevScene& S, float delta, uint32_t root, const Ray& r, float tmin, float& closest,
                     uint32_t& hit_code, uint32_t* stk, uint32_t mode) {
-    Trav T;
-    trav_init(T, S, root, root, r, tmin, closest, closest, 0u, mode);
-    while (trav_step(T, S, delta, stk)) {
+    const float tmax_entry = closest;
+    // A ray parallel to an axis plane (a zero direction component) can take the
+    // reference's NaN rect hit: t = (k - o) / d = 0 / 0 when the origin lies on
+    // the plane, and every comparison against NaN passes (rectangle.rs:36-65).
+    // No box bound covers that candidate, so such rays traverse unpruned.
+    const bool finite_slabs = r.d.x != 0.0f && r.d.y != 0.0f && r.d.z != 0.0f;
+    const bool prune = !(mode & kModeExact) && finite_slabs &&
+                       (__float_as_uint(S.nodes[4 * (size_t)root + 3].z) & rtdev::kBvhPrunable) != 0u;
+    const bool leaf_boxes = prune && !(mode & kModeNoLeafBoxes);
+    const V inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
+    const RayD q = to_d(r);
+    bool any = false;
+    uint32_t best_rank = 0, sp = 0, cur = root;
+    for (;;) {
+        const f4* nd = S.nodes + 4 * (size_t)cur;
+        f4 n0 = ld4(nd), n1 = ld4(nd + 1), n2 = ld4(nd + 2), n3 = ld4(nd + 3);
+        uint32_t lc = __float_as_uint(n3.x), rc = __float_as_uint(n3.y);
+        bool goL = false, goR = false;
+        float tl = 0.0f, tr = 0.0f;
+        PROF_T0(pt);
+        if (lc & rtdev::kLeafBit) {
+            if (!leaf_boxes || leaf_box_may_hit(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, r, inv, tmin, closest, delta)) {
+                PROF_T0(pl);
+                leaf_hit_ranked(S, lc, __float_as_uint(n3.z), r, q, tmin, closest, best_rank, hit_code, any);
+                PROF_ADD(kPrLeafTest, pl);
+            } else {
+                LEAF_AUDIT(lc, __float_as_uint(n3.z), n0.x, n0.y, n0.z, n0.w, n1.x, n1.y);
+            }
+        } else {
+            goL = slab(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, r, inv, tmin, tmax_entry, tl);
+            if (goL && prune) {
+                tl = slab_entry_inflated(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, r, inv, tmin, delta);
+                goL = !(tl > prune_bound(closest));
+            }
+        }
+        if (rc != rtdev::kChildEmpty) {
+            if (rc & rtdev::kLeafBit) {
+                if (!leaf_boxes ||
+                    leaf_box_may_hit(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, r, inv, tmin, closest, delta)) {
+                    PROF_T0(pl);
+                    leaf_hit_ranked(S, rc, __float_as_uint(n3.w), r, q, tmin, closest, best_rank, hit_code, any);
+                    PROF_ADD(kPrLeafTest, pl);
+                } else {
+                    LEAF_AUDIT(rc, __float_as_uint(n3.w), n1.z, n1.w, n2.x, n2.y, n2.z, n2.w);
+                }
+            } else {
+                goR = slab(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, r, inv, tmin, tmax_entry, tr);
+                if (goR && prune) {
+                    tr = slab_entry_inflated(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, r, inv, tmin, delta);
+                    goR = !(tr > prune_bound(closest));
+                }
+            }
+        }
+        PROF_ADD(kPrBvhTrip, pt);
+        if (goL && goR) {
+            bool left_first = tl <= tr;
+            uint32_t far = left_first ? rc : lc;
+            float tfar = left_first ? tr : tl;
+            cur = left_first ? lc : rc;
+            stk[sp * 128u] = far;
+            stk[sp * 128u + 64u] = __float_as_uint(tfar);
+            sp += 1u;
+            continue;
+        }
+        if (goL || goR) {
+            cur = goL ? lc : rc;
+            continue;
+        }
+        bool found = false;
+        while (sp > 0u) {
+            sp -= 1u;
+            uint32_t cand = stk[sp * 128u];
+            float tenter = __uint_as_float(stk[sp * 128u + 64u]);
+            if (!prune || !(tenter > prune_bound(closest))) {
+                cur = cand;
+                found = true;
+                break;
+            }
+        }
+        if (!found) break;
     }
-    closest = T.closest;
-    if (T.any) hit_code = T.hit_code;
-    return T.any;
+    return any;
 }
 
 // Translate (instance.rs:39) / RotateY (instance.rs:104-110, 121-124) applied to a ray.
@@ -694,36 +702,6 @@ RT_DEV bool medium_hit(const DevScene& S, float delta, const DevEntry* E, Ray r,
     if (hit_distance > distance_inside) return false;
     t_out = t1 + hit_distance / ray_length;
     return true;
-}
-
-// HittableList::hit over the world (hittable.rs:100-118), t in [0.001, inf).
-RT_DEV bool world_hit(const DevScene& S, float delta, const Ray& r, Rng& g, const Key& k, float& t_hit,
-                      uint32_t& hit_entry, uint32_t& hit_code, uint32_t* stk, uint32_t exact) {
-    float closest = kInf;
-    bool any = false;
-    for (uint32_t e = 0; e < S.num_top; ++e) {
-        const DevEntry* E = S.entries + e;
-        PROF_T0(pe);
-        if (E->kind == rtdev::kEntMedium) {
-            float t;
-            if (medium_hit(S, delta, E, r, 0.001f, closest, g, k, t, stk, exact)) {
-                closest = t;
-                hit_entry = e;
-                hit_code = rtdev::leaf_code(rtdev::kLeafMedium, 0);
-                any = true;
-            }
-        } else {
-            uint32_t code;
-            if (entry_geom_hit(S, delta, E, r, 0.001f, closest, code, stk, exact)) {
-                hit_entry = e;
-                hit_code = code;
-                any = true;
-            }
-        }
-        PROF_ADD(kPrEntry0 + (e < kPrBvhTrip - kPrEntry0 - 1 ? e : kPrBvhTrip - kPrEntry0 - 1), pe);
-    }
-    t_hit = closest;
-    return any;
 }
 
 // ---------------------------------------------------------------------------
@@ -1043,6 +1021,36 @@ struct ChunkParams {
     uint32_t npix;            // width * height (sample-buffer plane size)
 };
 
+// HittableList::hit over the world (hittable.rs:100-118), t in [0.001, inf).
+RT_DEV bool world_hit(const DevScene& S, float delta, const Ray& r, Rng& g, const Key& k, float& t_hit,
+                      uint32_t& hit_entry, uint32_t& hit_code, uint32_t* stk, uint32_t mode) {
+    float closest = kInf;
+    bool any = false;
+    for (uint32_t e = 0; e < S.num_top; ++e) {
+        const DevEntry* E = S.entries + e;
+        PROF_T0(pe);
+        if (E->kind == rtdev::kEntMedium) {
+            float t;
+            if (medium_hit(S, delta, E, r, 0.001f, closest, g, k, t, stk, mode)) {
+                closest = t;
+                hit_entry = e;
+                hit_code = rtdev::leaf_code(rtdev::kLeafMedium, 0);
+                any = true;
+            }
+        } else {
+            uint32_t code;
+            if (entry_geom_hit(S, delta, E, r, 0.001f, closest, code, stk, mode)) {
+                hit_entry = e;
+                hit_code = code;
+                any = true;
+            }
+        }
+        PROF_ADD(e < kPrEntryLast - kPrEntry0 ? kPrEntry0 + e : kPrEntryLast, pe);
+    }
+    t_hit = closest;
+    return any;
+}
+
 // Renderer::get_color's sample loop (renderer.rs:140-146) as a work pool. Each
 // lane owns one camera sample at a time; when its path ends (ray.rs:32-62) it
 // stores the sample's radiance in the HBM sample buffer and takes the next item.
@@ -1050,551 +1058,148 @@ struct ChunkParams {
 // a batch costs one atomic, so no lane waits for a neighbour's long path.
 // resolve_samples() then sums every pixel's samples IN SAMPLE ORDER, exactly like
 // `color_accumulator +=` in the reference.
+struct ItemPool {  // wave-uniform
+    uint32_t batch, next, end;
+    bool exhausted;
+};
+// Gives the next work item to every lane with `want` set. A lane that got a
+// sample returns true with its camera ray started (renderer.rs:141-143); a
+// max_depth 0 sample (ray.rs:39-41: black, no segment) is stored and skipped.
+RT_DEV bool take_sample(ItemPool& pool, bool want, const DevCamera& C, const DevParams& P, const ChunkParams& Q,
+                        const Key& k, unsigned* batch_counter, float* sbuf, uint32_t lane, uint32_t& pixel,
+                        uint32_t& s_local, V& L, V& T, uint32_t& depth, Rng& g, Ray& ray) {
+    bool got = false;
+    for (;;) {
+        unsigned long long need = __ballot(want && !got);
+        if (need == 0ull || pool.exhausted) break;
+        if (pool.next == pool.end) {
+            uint32_t bt = 0;
+            if (lane == 0u) bt = atomicAdd(batch_counter, 1u);
+            bt = __builtin_amdgcn_readfirstlane(bt);
+            if (bt >= Q.num_batches) {
+                pool.exhausted = true;
+                break;
+            }
+            pool.batch = bt;
+            pool.next = 0u;
+            pool.end = 64u * kGroup;
+            continue;
+        }
+        uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
+        uint32_t avail = pool.end - pool.next;
+        if (want && !got && rank < avail) {
+            uint32_t item = pool.next + rank;
+            uint32_t blk_local = pool.batch / Q.groups_per_block;
+            uint32_t grp = pool.batch - blk_local * Q.groups_per_block;
+            uint32_t s = grp * kGroup + (item >> 6);
+            uint32_t pib = item & 63u;
+            uint32_t blk = P.shard_index + blk_local * P.shard_count;
+            uint32_t by = blk / P.blocks_x, bx = blk - by * P.blocks_x;
+            uint32_t x = bx * 8u + (pib & 7u), y = by * 8u + (pib >> 3);
+            if (x < P.width && y < P.height && s < Q.samples) {
+                pixel = y * P.width + x;
+                s_local = s;
+                L = mk(0.0f, 0.0f, 0.0f);
+                T = mk(1.0f, 1.0f, 1.0f);
+                depth = P.max_depth;
+                start_sample(C, P, k, x, y, pixel, Q.sample0 + s, g, ray);
+                if (depth == 0u) {
+                    float* o = sbuf + ((size_t)s_local * Q.npix + pixel) * 3u;
+                    o[0] = o[1] = o[2] = 0.0f;
+                } else {
+                    got = true;
+                }
+            }
+        }
+        uint32_t n = (uint32_t)__popcll(need);
+        pool.next += n < avail ? n : avail;
+    }
+    return got;
+}
+
+// The end of a segment whose list walk is complete (ray.rs:43-61): background,
+// or HitRecord + emit + scatter. Returns true when the path ends; its radiance is
+// then stored in the sample buffer.
+RT_DEV bool finish_segment(const DevScene& S, const DevParams& P, const ChunkParams& Q, const Key& k,
+                           float* __restrict__ sbuf, bool any, uint32_t he, uint32_t hc, float t, Ray& ray, V& L, V& T,
+                           uint32_t& depth, Rng& g, uint32_t pixel, uint32_t s_local) {
+    PROF_T0(pg);
+    bool done;
+    if (!any) {
+        L = L + T * mk(P.bg[0], P.bg[1], P.bg[2]);
+        done = true;
+    } else {
+        Rec rec;
+        PROF_T0(pc);
+        make_record(S, he, hc, t, ray, rec);
+        PROF_ADD(kPrRecord, pc);
+        const DevMaterial m = S.mats[rec.mat];
+        PROF_T0(pm);
+        V em = m.kind == rtdev::kMatLight ? tex_value(S, m.tex, rec.u, rec.v, rec.p) : mk(0.0f, 0.0f, 0.0f);
+        L = L + T * em;
+        PROF_ADD(kPrEmit, pm);
+        V att;
+        Ray sc;
+        PROF_T0(ps);
+        bool scattered = scatter(S, m, ray, rec, g, k, att, sc);
+        PROF_ADD(kPrScatter, ps);
+        if (scattered) {
+            T = T * att;
+            ray = sc;
+            depth -= 1u;
+            done = depth == 0u;
+        } else {
+            done = true;
+        }
+    }
+    if (done) {
+        float* o = sbuf + ((size_t)s_local * Q.npix + pixel) * 3u;
+        o[0] = L.x;
+        o[1] = L.y;
+        o[2] = L.z;
+    }
+    PROF_ADD(kPrSegment, pg);
+    return done;
+}
+
+// Every live lane traces one whole segment per loop trip: the list walk with its
+// BVH traversals inline, then finish_segment.
 __global__ __launch_bounds__(64) void trace_samples(DevScene S, DevCamera C, DevParams P, ChunkParams Q,
-                                                     float* __restrict__ sbuf, unsigned* __restrict__ batch_counter,
-                                                     unsigned long long* __restrict__ seg_counter) {
+                                                    float* __restrict__ sbuf, unsigned* __restrict__ batch_counter,
+                                                    unsigned long long* __restrict__ seg_counter) {
     extern __shared__ uint32_t lds_stack[];
     const uint32_t lane = threadIdx.x;
     uint32_t* stk = lds_stack + lane;  // [level][{node, t_enter}][lane]
     const Key k{P.seed_lo, P.seed_hi};
-    const uint32_t exact = ((P.flags & RT_FLAG_EXACT_BVH) ? kModeExact : 0u) | P.tune;
-    const V bg = mk(P.bg[0], P.bg[1], P.bg[2]);
-
+    const uint32_t mode = ((P.flags & RT_FLAG_EXACT_BVH) ? kModeExact : 0u) | P.tune;
     bool has = false;
     uint32_t pixel = 0, s_local = 0, depth = 0, nseg = 0;
     V L = mk(0.0f, 0.0f, 0.0f), T = mk(1.0f, 1.0f, 1.0f);
-    Rng g;
-    g.sample = g.pixel = g.block = g.n = 0u;
-    g.b0 = g.b1 = g.b2 = g.b3 = 0u;
-    Ray ray;
-    ray.o = ray.d = mk(0.0f, 0.0f, 0.0f);
-    ray.time = 0.0f;
-    uint32_t pool_batch = 0, pool_next = 0, pool_end = 0;  // wave-uniform
-    bool exhausted = false;                                 // wave-uniform
+    Rng g{};
+    Ray ray{};
+    ItemPool pool{0u, 0u, 0u, false};
     PROF_INIT();
-
     for (;;) {
-        // ---- hand items to idle lanes ------------------------------------
         PROF_T0(pr);
-        for (;;) {
-            unsigned long long need = __ballot(!has);
-            if (need == 0ull || exhausted) break;
-            if (pool_next == pool_end) {
-                uint32_t bt = 0;
-                if (lane == 0u) bt = atomicAdd(batch_counter, 1u);
-                bt = __builtin_amdgcn_readfirstlane(bt);
-                if (bt >= Q.num_batches) {
-                    exhausted = true;
-                    break;
-                }
-                pool_batch = bt;
-                pool_next = 0u;
-                pool_end = 64u * kGroup;
-                continue;
-            }
-            uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
-                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
-            uint32_t avail = pool_end - pool_next;
-            if (!has && rank < avail) {
-                uint32_t item = pool_next + rank;
-                uint32_t blk_local = pool_batch / Q.groups_per_block;
-                uint32_t grp = pool_batch - blk_local * Q.groups_per_block;
-                uint32_t s = grp * kGroup + (item >> 6);
-                uint32_t pib = item & 63u;
-                uint32_t blk = P.shard_index + blk_local * P.shard_count;
-                uint32_t by = blk / P.blocks_x, bx = blk - by * P.blocks_x;
-                uint32_t x = bx * 8u + (pib & 7u), y = by * 8u + (pib >> 3);
-                if (x < P.width && y < P.height && s < Q.samples) {
-                    has = true;
-                    pixel = y * P.width + x;
-                    s_local = s;
-                    L = mk(0.0f, 0.0f, 0.0f);
-                    T = mk(1.0f, 1.0f, 1.0f);
-                    depth = P.max_depth;
-                    start_sample(C, P, k, x, y, pixel, Q.sample0 + s, g, ray);
-                }
-            }
-            uint32_t n = (uint32_t)__popcll(need);
-            pool_next += n < avail ? n : avail;
-        }
+        if (take_sample(pool, !has, C, P, Q, k, batch_counter, sbuf, lane, pixel, s_local, L, T, depth, g, ray))
+            has = true;
         PROF_ADD(kPrRefill, pr);
         if (__ballot(has) == 0ull) break;  // pool exhausted and every path finished
-
-        // ---- one ray segment per live lane (ray.rs:32-62) -----------------
         if (has) {
-            PROF_T0(pg);
-            bool done;
-            if (depth == 0u) {
-                done = true;  // ray.rs:39-41
-            } else {
-                nseg += 1u;
-                float t;
-                uint32_t entry = 0, code = 0;
-                PROF_T0(pw);
-                bool hit = world_hit(S, P.prune_delta, ray, g, k, t, entry, code, stk, exact);
-                PROF_ADD(kPrWorld, pw);
-                if (!hit) {
-                    L = L + T * bg;
-                    done = true;
-                } else {
-                    Rec rec;
-                    PROF_T0(pc);
-                    make_record(S, entry, code, t, ray, rec);
-                    PROF_ADD(kPrRecord, pc);
-                    const DevMaterial m = S.mats[rec.mat];
-                    PROF_T0(pe);
-                    V e = m.kind == rtdev::kMatLight ? tex_value(S, m.tex, rec.u, rec.v, rec.p) : mk(0.0f, 0.0f, 0.0f);
-                    L = L + T * e;
-                    PROF_ADD(kPrEmit, pe);
-                    V att;
-                    Ray sc;
-                    PROF_T0(ps);
-                    bool scattered = scatter(S, m, ray, rec, g, k, att, sc);
-                    PROF_ADD(kPrScatter, ps);
-                    if (scattered) {
-                        T = T * att;
-                        ray = sc;
-                        depth -= 1u;
-                        done = depth == 0u;
-                    } else {
-                        done = true;
-                    }
-                }
-            }
-            if (done) {
-                PROF_T0(po);
-                float* o = sbuf + ((size_t)s_local * Q.npix + pixel) * 3u;
-                o[0] = L.x;
-                o[1] = L.y;
-                o[2] = L.z;
-                has = false;
-                PROF_ADD(kPrStore, po);
-            }
-            PROF_ADD(kPrSegment, pg);
+            nseg += 1u;
+            float t;
+            uint32_t he = 0, hc = 0;
+            PROF_T0(pw);
+            bool any = world_hit(S, P.prune_delta, ray, g, k, t, he, hc, stk, mode);
+            PROF_ADD(kPrWorld, pw);
+            if (finish_segment(S, P, Q, k, sbuf, any, he, hc, t, ray, L, T, depth, g, pixel, s_local)) has = false;
         }
     }
-    PROF_FLUSH();
     if (seg_counter) {
         unsigned long long v = nseg;
         for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
         if (lane == 0u) atomicAdd(seg_counter, v);
     }
-}
-
-// ---------------------------------------------------------------------------
-// Wavefront path (scenes with top-level BVHs). The megakernel above keeps one
-// path per lane for its whole life, so a wave pays for its slowest lane inside
-// every BVH: measured 5 of 64 lanes active per traversal step on C3. Here path
-// state lives in an HBM pool (80 B per slot) and every bounce runs as
-//   wf_logic  shade the previous hit (emit / scatter), finish + regenerate,
-//             then the entries of pass 0 inline;
-//   wf_bvh    per pass: persistent traversal of the queued (slot, BVH) work,
-//             a lane takes the next ray the moment its own finishes;
-//   wf_pass   passes > 0: the next run of inline entries.
-// A pass is a run of top-level entries; its BVHs are queued, everything else is
-// tested inline. Geometry entries commute under the (t, entry, DFS rank) tie
-// rule, and a BVH's reference box tests use the t_max recorded when the inline
-// walk passed it in list order. A ConstantMedium draws its ln(U) only if its
-// clamped interval is non-empty against closest-so-far, so a pass ends before
-// any medium preceded by a queued BVH of the same pass: media always see the
-// exact list-order closest. Same draws, same candidates, same winner.
-// ---------------------------------------------------------------------------
-constexpr uint32_t kMaxPasses = 8, kMaxPassBvh = 8;
-constexpr uint32_t kNoHit = 0xffffffffu;
-constexpr uint32_t kStFree = 0u, kStTrace = 1u;
-struct WfPass {
-    uint32_t first, last;  // inline top-level entries [first, last)
-    uint32_t nbvh;         // queued BVH entries (ascending) of this pass
-    uint32_t bvh[kMaxPassBvh];
-};
-struct WfPlan {
-    uint32_t npass;
-    WfPass pass[kMaxPasses];
-};
-// counters: two sets alternate by iteration parity (a set is zeroed by the logic
-// kernel of the previous iteration); the item counter is per chunk.
-enum : uint32_t { kCtrTrace = 0, kCtrActive = 1, kCtrQueue = 2, kCtrPull = 2 + kMaxPasses, kCtrStride = 32 };
-constexpr uint32_t kCtrItems = 2 * kCtrStride;
-struct WfPool {
-    f4* o;            // o.xyz, time
-    f4* d;            // d.xyz, closest
-    f4* tl;           // T.xyz, L.x
-    f4* lh;           // L.y, L.z, hit entry, hit code (bits)
-    uint4* m;         // pixel, chunk sample, depth | status << 16, rng block << 3 | n
-    float* tmax;      // [kMaxPassBvh][np]: t_max when the inline walk reached the BVH
-    uint32_t* trace;  // slots tracing this iteration (passes > 0 walk this list)
-    uint2* queue;     // (slot, BVH bit mask) for the current pass
-    uint32_t* ctr;
-    uint32_t np;
-};
-
-RT_DEV void rng_resume(Rng& g, uint32_t packed, uint32_t sample, uint32_t pixel, const Key& k) {
-    g.sample = sample;
-    g.pixel = pixel;
-    g.block = packed >> 3;
-    g.n = packed & 7u;
-    g.b0 = g.b1 = g.b2 = g.b3 = 0u;
-    if (g.n != 0u) {  // the cached block: recompute it, drop the 4 - n values already drawn
-        uint4 b = philox_block(g.block - 1u, sample, pixel, k.k0, k.k1);
-        if (g.n == 3u) { g.b0 = b.y; g.b1 = b.z; g.b2 = b.w; }
-        else if (g.n == 2u) { g.b0 = b.z; g.b1 = b.w; }
-        else { g.b0 = b.w; }
-    }
-}
-RT_DEV uint32_t rng_pack(const Rng& g) { return (g.block << 3) | g.n; }
-
-// Inline entries of one pass for one ray (hittable.rs:100-118 in list order).
-// Returns the mask of queued BVHs whose root box the ray enters, with their
-// list-order t_max in tmax[j * np + slot].
-RT_DEV uint32_t wf_inline(const DevScene& S, const DevParams& P, const WfPass& ps, const Ray& ray, Rng& g,
-                          const Key& k, float& closest, uint32_t& he, uint32_t& hc, float* tmax, uint32_t np,
-                          uint32_t slot, uint32_t* stk, uint32_t mode) {
-    uint32_t mask = 0u, j = 0u;
-    for (uint32_t e = ps.first; e < ps.last; ++e) {
-        const DevEntry* E = S.entries + e;
-        if (E->kind == rtdev::kEntMedium) {
-            float t;
-            if (medium_hit(S, P.prune_delta, E, ray, 0.001f, closest, g, k, t, stk, mode)) {
-                closest = t;
-                he = e;
-                hc = rtdev::leaf_code(rtdev::kLeafMedium, 0);
-            }
-        } else if (j < ps.nbvh && ps.bvh[j] == e) {
-            // the wrapper node's child box = the root box, tested like bvh.rs:370
-            Ray r = ray;
-            for (uint32_t i = 0; i < E->ntf; ++i) r = apply_op(E->tf[i], r);
-            const f4* nd = S.nodes + 4 * (size_t)E->payload;
-            f4 n0 = ld4(nd), n1 = ld4(nd + 1), n3 = ld4(nd + 3);
-            V inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
-            float te;
-            bool go = slab(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, r, inv, 0.001f, closest, te);
-            if (go && !(mode & kModeExact) && (__float_as_uint(n3.z) & rtdev::kBvhPrunable)) {
-                te = slab_entry_inflated(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, r, inv, 0.001f, P.prune_delta);
-                go = !(te > prune_bound(closest));
-            }
-            if (go) {
-                mask |= 1u << j;
-                tmax[(size_t)j * np + slot] = closest;
-            }
-            ++j;
-        } else {
-            uint32_t code;
-            if (entry_geom_hit(S, P.prune_delta, E, ray, 0.001f, closest, code, stk, mode)) {
-                he = e;
-                hc = code;
-            }
-        }
-    }
-    return mask;
-}
-
-// Wave-aggregated append of (slot, mask) to the pass queue.
-RT_DEV void wf_enqueue(const WfPool& W, uint32_t* ctr, uint32_t pass, uint32_t slot, uint32_t mask) {
-    unsigned long long b = __ballot(mask != 0u);
-    if (b == 0ull) return;
-    uint32_t lane = __lane_id();
-    uint32_t first = (uint32_t)__builtin_ctzll(b);
-    uint32_t base = 0;
-    if (lane == first) base = atomicAdd(&ctr[kCtrQueue + pass], (uint32_t)__popcll(b));
-    base = __shfl(base, (int)first);
-    if (mask != 0u) {
-        uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
-        W.queue[base + rank] = make_uint2(slot, mask);
-    }
-}
-RT_DEV void wf_append_trace(const WfPool& W, uint32_t* ctr, uint32_t slot, bool on) {
-    unsigned long long b = __ballot(on);
-    if (b == 0ull) return;
-    uint32_t lane = __lane_id();
-    uint32_t first = (uint32_t)__builtin_ctzll(b);
-    uint32_t base = 0;
-    if (lane == first) base = atomicAdd(&ctr[kCtrTrace], (uint32_t)__popcll(b));
-    base = __shfl(base, (int)first);
-    if (on) {
-        uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
-        W.trace[base + rank] = slot;
-    }
-}
-
-// Item -> (pixel, chunk sample): the megakernel's order (8x8 block, group of
-// kGroup samples, sample, pixel-in-block), so consecutive items are neighbours.
-RT_DEV bool wf_item(const DevParams& P, const ChunkParams& Q, uint32_t item, uint32_t& x, uint32_t& y,
-                    uint32_t& s) {
-    uint32_t batch = item / (64u * kGroup), within = item - batch * (64u * kGroup);
-    uint32_t blk_local = batch / Q.groups_per_block;
-    uint32_t grp = batch - blk_local * Q.groups_per_block;
-    s = grp * kGroup + (within >> 6);
-    uint32_t pib = within & 63u;
-    uint32_t blk = P.shard_index + blk_local * P.shard_count;
-    uint32_t by = blk / P.blocks_x, bx = blk - by * P.blocks_x;
-    x = bx * 8u + (pib & 7u);
-    y = by * 8u + (pib >> 3);
-    return x < P.width && y < P.height && s < Q.samples;
-}
-
-__global__ __launch_bounds__(64) void wf_logic(DevScene S, DevCamera C, DevParams P, ChunkParams Q, WfPool W,
-                                               const WfPlan* __restrict__ plan, uint32_t parity,
-                                               float* __restrict__ sbuf,
-                                               unsigned long long* __restrict__ seg_counter) {
-    extern __shared__ uint32_t lds_stack[];
-    const uint32_t lane = threadIdx.x;
-    uint32_t* stk = lds_stack + lane;
-    const uint32_t slot = blockIdx.x * 64u + lane;  // np is a multiple of 64
-    PROF_INIT();
-    PROF_T0(pw);
-    uint32_t* ctr = W.ctr + parity * kCtrStride;
-    if (blockIdx.x == 0u && lane < kCtrStride) W.ctr[(parity ^ 1u) * kCtrStride + lane] = 0u;
-    const Key k{P.seed_lo, P.seed_hi};
-    const uint32_t mode = ((P.flags & RT_FLAG_EXACT_BVH) ? kModeExact : 0u) | P.tune;
-
-    uint4 m = W.m[slot];
-    uint32_t status = m.z >> 16, depth = m.z & 0xffffu;
-    Rng g;
-    Ray ray;
-    V T = mk(1.0f, 1.0f, 1.0f), L = mk(0.0f, 0.0f, 0.0f);
-    bool dirty = false;
-    PROF_T0(ps);
-    if (status == kStTrace) {  // shade the segment traced last iteration (ray.rs:43-61)
-        f4 o = W.o[slot], d = W.d[slot], tl = W.tl[slot], lh = W.lh[slot];
-        ray.o = xyz(o);
-        ray.time = o.w;
-        ray.d = xyz(d);
-        T = xyz(tl);
-        L = mk(tl.w, lh.x, lh.y);
-        rng_resume(g, m.w, Q.sample0 + m.y, m.x, k);
-        uint32_t he = __float_as_uint(lh.z), hc = __float_as_uint(lh.w);
-        bool done;
-        if (he == kNoHit) {
-            L = L + T * mk(P.bg[0], P.bg[1], P.bg[2]);
-            done = true;
-        } else {
-            Rec rec;
-            make_record(S, he, hc, d.w, ray, rec);
-            const DevMaterial mt = S.mats[rec.mat];
-            V e = mt.kind == rtdev::kMatLight ? tex_value(S, mt.tex, rec.u, rec.v, rec.p) : mk(0.0f, 0.0f, 0.0f);
-            L = L + T * e;
-            V att;
-            Ray sc;
-            if (scatter(S, mt, ray, rec, g, k, att, sc)) {
-                T = T * att;
-                ray = sc;
-                depth -= 1u;
-                done = depth == 0u;
-            } else {
-                done = true;
-            }
-        }
-        if (done) {
-            float* out = sbuf + ((size_t)m.y * Q.npix + m.x) * 3u;
-            out[0] = L.x;
-            out[1] = L.y;
-            out[2] = L.z;
-            status = kStFree;
-        }
-        dirty = true;
-        PROF_ADD(kPrWfShade, ps);
-    }
-    // regenerate: idle slots take the next camera samples (renderer.rs:140-146)
-    PROF_T0(pr);
-    const uint32_t total_items = Q.num_batches * 64u * kGroup;
-    for (;;) {
-        unsigned long long need = __ballot(status == kStFree);
-        if (need == 0ull) break;
-        // once exhausted, stop adding to the counter (keeps it from wrapping)
-        if (__hip_atomic_load(&W.ctr[kCtrItems], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= total_items) break;
-        uint32_t first = (uint32_t)__builtin_ctzll(need);
-        uint32_t base = 0;
-        if (lane == first) base = atomicAdd(&W.ctr[kCtrItems], (uint32_t)__popcll(need));
-        base = __shfl(base, (int)first);
-        if (base >= total_items) break;  // items exhausted (wave-uniform)
-        if (status == kStFree) {
-            uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
-                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
-            uint32_t item = base + rank, x, y, s;
-            if (item < total_items && wf_item(P, Q, item, x, y, s)) {
-                m.x = y * P.width + x;
-                m.y = s;
-                T = mk(1.0f, 1.0f, 1.0f);
-                L = mk(0.0f, 0.0f, 0.0f);
-                start_sample(C, P, k, x, y, m.x, Q.sample0 + s, g, ray);
-                depth = P.max_depth;
-                dirty = true;
-                if (depth == 0u) {  // ray.rs:39-41: no segment, black sample
-                    float* out = sbuf + ((size_t)s * Q.npix + m.x) * 3u;
-                    out[0] = out[1] = out[2] = 0.0f;
-                } else {
-                    status = kStTrace;
-                }
-            }
-        }
-    }
-    PROF_ADD(kPrWfRegen, pr);
-    const bool trace = status == kStTrace;
-    float closest = kInf;
-    uint32_t he = kNoHit, hc = 0u, mask = 0u;
-    PROF_T0(pi);
-    if (trace) mask = wf_inline(S, P, plan->pass[0], ray, g, k, closest, he, hc, W.tmax, W.np, slot, stk, mode);
-    PROF_ADD(kPrWfInline, pi);
-    PROF_T0(pt);
-    if (dirty || trace) {
-        W.m[slot] = make_uint4(m.x, m.y, depth | (status << 16), rng_pack(g));
-        if (trace) {
-            W.o[slot] = f4{ray.o.x, ray.o.y, ray.o.z, ray.time};
-            W.d[slot] = f4{ray.d.x, ray.d.y, ray.d.z, closest};
-            W.tl[slot] = f4{T.x, T.y, T.z, L.x};
-            W.lh[slot] = f4{L.y, L.z, __uint_as_float(he), __uint_as_float(hc)};
-        }
-    }
-    if (plan->pass[0].nbvh) wf_enqueue(W, ctr, 0u, slot, mask);
-    if (plan->npass > 1u) wf_append_trace(W, ctr, slot, trace);
-    unsigned long long tb = __ballot(trace);
-    if (lane == 0u && tb) {
-        atomicAdd(&ctr[kCtrActive], (uint32_t)__popcll(tb));
-        if (seg_counter) atomicAdd(seg_counter, (unsigned long long)__popcll(tb));
-    }
-    PROF_ADD(kPrWfTail, pt);
-    PROF_ADD(kPrWfLogicWave, pw);
-    PROF_FLUSH();
-}
-
-// Passes > 0: the next run of inline entries for every tracing slot.
-__global__ __launch_bounds__(64) void wf_pass(DevScene S, DevParams P, ChunkParams Q, WfPool W,
-                                              const WfPlan* __restrict__ plan, uint32_t pass, uint32_t parity) {
-    extern __shared__ uint32_t lds_stack[];
-    const uint32_t lane = threadIdx.x;
-    uint32_t* stk = lds_stack + lane;
-    uint32_t* ctr = W.ctr + parity * kCtrStride;
-    const uint32_t n = ctr[kCtrTrace];
-    const Key k{P.seed_lo, P.seed_hi};
-    const uint32_t mode = ((P.flags & RT_FLAG_EXACT_BVH) ? kModeExact : 0u) | P.tune;
-    const WfPass& ps = plan->pass[pass];
-    PROF_INIT();
-    PROF_T0(pw);
-    for (uint32_t i0 = blockIdx.x * 64u; i0 < n; i0 += gridDim.x * 64u) {
-        uint32_t i = i0 + lane;
-        bool on = i < n;
-        uint32_t slot = on ? W.trace[i] : 0u, mask = 0u;
-        if (on) {
-            f4 o = W.o[slot], d = W.d[slot], lh = W.lh[slot];
-            uint4 m = W.m[slot];
-            Ray ray;
-            ray.o = xyz(o);
-            ray.time = o.w;
-            ray.d = xyz(d);
-            Rng g;
-            rng_resume(g, m.w, Q.sample0 + m.y, m.x, k);
-            float closest = d.w;
-            uint32_t he = __float_as_uint(lh.z), hc = __float_as_uint(lh.w);
-            uint32_t n0 = g.block * 8u + g.n;
-            mask = wf_inline(S, P, ps, ray, g, k, closest, he, hc, W.tmax, W.np, slot, stk, mode);
-            if (closest != d.w || he != __float_as_uint(lh.z) || hc != __float_as_uint(lh.w)) {
-                W.d[slot].w = closest;
-                W.lh[slot] = f4{lh.x, lh.y, __uint_as_float(he), __uint_as_float(hc)};
-            }
-            if (g.block * 8u + g.n != n0) W.m[slot].w = rng_pack(g);
-        }
-        if (ps.nbvh) wf_enqueue(W, ctr, pass, slot, on ? mask : 0u);
-    }
-    PROF_ADD(kPrWfPassWave, pw);
-    PROF_FLUSH();
-}
-
-// Set up the traversal of the lowest BVH bit of `mask` for `slot`; returns its entry.
-RT_DEV uint32_t wf_job_start(Trav& T, const DevScene& S, const WfPool& W, const WfPass& ps, uint32_t slot,
-                             uint32_t mask, float closest, uint32_t he, uint32_t mode) {
-    uint32_t j = (uint32_t)__builtin_ctz(mask);
-    uint32_t e = ps.bvh[j];
-    const DevEntry* E = S.entries + e;
-    f4 o = W.o[slot], d = W.d[slot];
-    Ray r;
-    r.o = xyz(o);
-    r.time = o.w;
-    r.d = xyz(d);
-    for (uint32_t i = 0; i < E->ntf; ++i) r = apply_op(E->tf[i], r);
-    uint32_t wrapper = E->payload;
-    uint32_t root = __float_as_uint(S.nodes[4 * (size_t)wrapper + 3].x);
-    uint32_t best_rank = (he != kNoHit && he > e) ? 0xffffffffu : 0u;
-    trav_init(T, S, wrapper, root, r, 0.001f, W.tmax[(size_t)j * W.np + slot], closest, best_rank, mode);
-    return e;
-}
-
-// Persistent traversal of the pass queue: each lane owns one (slot, BVH) job at a
-// time and takes the next job as soon as its traversal ends, so lanes do not
-// wait for the slowest ray of their wave.
-__global__ __launch_bounds__(64, 5) void wf_bvh(DevScene S, DevParams P, WfPool W, const WfPlan* __restrict__ plan,
-                                             uint32_t pass, uint32_t parity) {
-    extern __shared__ uint32_t lds_stack[];
-    const uint32_t lane = threadIdx.x;
-    uint32_t* stk = lds_stack + lane;
-    uint32_t* ctr = W.ctr + parity * kCtrStride;
-    const uint32_t qn = ctr[kCtrQueue + pass];
-    const uint32_t mode = ((P.flags & RT_FLAG_EXACT_BVH) ? kModeExact : 0u) | P.tune;
-    const WfPass& ps = plan->pass[pass];
-
-    bool has = false;
-    uint32_t slot = 0, mask = 0, e = 0, he = kNoHit, hc = 0, he0 = kNoHit;
-    float closest0 = kInf;
-    Trav T;
-    uint32_t pool_next = 0, pool_end = 0;  // wave-uniform: this wave's share of the queue
-    bool exhausted = false;
-    PROF_INIT();
-    PROF_T0(pw);
-
-
-    for (;;) {
-        unsigned long long need = __ballot(!has);
-        PROF_T0(pf);
-        while (need != 0ull && !exhausted) {
-            if (pool_next == pool_end) {
-                uint32_t b = 0;
-                if (lane == 0u) b = atomicAdd(&ctr[kCtrPull + pass], 64u);
-                b = __builtin_amdgcn_readfirstlane(b);
-                if (b >= qn) {
-                    exhausted = true;
-                    break;
-                }
-                pool_next = b;
-                pool_end = b + 64u < qn ? b + 64u : qn;
-            }
-            uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
-                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
-            uint32_t avail = pool_end - pool_next;
-            if (!has && rank < avail) {
-                uint2 q = W.queue[pool_next + rank];
-                slot = q.x;
-                mask = q.y;
-                f4 lh = W.lh[slot];
-                he0 = he = __float_as_uint(lh.z);
-                hc = __float_as_uint(lh.w);
-                closest0 = W.d[slot].w;
-                e = wf_job_start(T, S, W, ps, slot, mask, closest0, he, mode);
-                has = true;
-            }
-            uint32_t taken = (uint32_t)__popcll(need);
-            pool_next += taken < avail ? taken : avail;
-            need = __ballot(!has);
-        }
-        PROF_ADD(kPrWfBvhRefill, pf);
-        if (__ballot(has) == 0ull) break;
-        if (has && !trav_step(T, S, P.prune_delta, stk)) {
-            if (T.any) {
-                he = e;
-                hc = T.hit_code;
-            }
-            mask &= mask - 1u;
-            if (mask != 0u) {
-                e = wf_job_start(T, S, W, ps, slot, mask, T.closest, he, mode);  // closest carries over
-            } else {
-                if (he != he0 || T.closest != closest0 || T.any) {
-                    W.d[slot].w = T.closest;
-                    f4 lh = W.lh[slot];
-                    W.lh[slot] = f4{lh.x, lh.y, __uint_as_float(he), __uint_as_float(hc)};
-                }
-                has = false;
-            }
-        }
-    }
-    PROF_ADD(kPrWfBvhWave, pw);
     PROF_FLUSH();
 }
 
@@ -1659,22 +1264,11 @@ struct rt_scene {
     unsigned* counter = nullptr;
     int grid = 0;  // resident waves of trace_samples
     float coord_bound = 0.0f;
-    // HIP events bracketing every trace_samples launch (rt_scene_trace_time)
+    // HIP events bracketing every trace launch (rt_scene_trace_time)
     static constexpr int kEvents = 256;
     hipEvent_t ev[kEvents][2] = {};
     int ev_count = 0;
     bool ev_overflow = false;
-    // wavefront path (scenes with top-level BVHs): plan, path pool, round sync
-    WfPlan plan{};
-    WfPlan* d_plan = nullptr;  // device copy (kernels index it dynamically)
-    bool wf = false;
-    uint32_t max_pass_bvh = 0;
-    void* wf_mem = nullptr;
-    uint32_t wf_np = 0;  // slots the pool was allocated for
-    WfPool wp{};
-    uint32_t* h_active = nullptr;  // pinned, one per round parity
-    hipEvent_t round_ev[2] = {};
-    int grid_pass = 0, grid_bvh = 0;
 };
 
 namespace {
@@ -1732,144 +1326,6 @@ int rt_device_count(int* count) {
     *count = n;
     return RT_OK;
 }
-
-namespace {
-
-// Split the top-level list into passes (see the wavefront notes above): every
-// top-level BVH is queued; a pass ends before a medium that follows a queued
-// BVH of the same pass, or when a pass holds kMaxPassBvh BVHs.
-bool build_plan(const rthost::HostScene& hs, WfPlan* plan, uint32_t* max_bvh) {
-    memset(plan, 0, sizeof *plan);
-    *max_bvh = 0;
-    WfPass cur{};
-    uint32_t n = 0, nbvh_total = 0;
-    auto close = [&](uint32_t last) {
-        cur.last = last;
-        if (n < kMaxPasses) plan->pass[n] = cur;
-        ++n;
-        if (cur.nbvh > *max_bvh) *max_bvh = cur.nbvh;
-        cur = WfPass{};
-        cur.first = last;
-    };
-    for (uint32_t e = 0; e < hs.num_top; ++e) {
-        uint32_t kind = hs.entries[e].kind;
-        if ((kind == rtdev::kEntMedium && cur.nbvh > 0) || (kind == rtdev::kEntBvh && cur.nbvh == kMaxPassBvh))
-            close(e);
-        if (kind == rtdev::kEntBvh) {
-            cur.bvh[cur.nbvh++] = e;
-            ++nbvh_total;
-        }
-    }
-    close(hs.num_top);
-    plan->npass = n;
-    return n <= kMaxPasses && nbvh_total > 0;
-}
-
-int wf_alloc(rt_scene* s, uint32_t np) {
-    if (s->wf_np >= np && s->wf_mem) return RT_OK;
-    if (s->wf_mem) (void)hipFree(s->wf_mem);
-    s->wf_mem = nullptr;
-    s->wf_np = 0;
-    const uint64_t nb = s->max_pass_bvh ? s->max_pass_bvh : 1u;
-    const uint64_t sizes[] = {16ull * np, 16ull * np, 16ull * np, 16ull * np, 16ull * np, 4ull * nb * np,
-                              4ull * np, 8ull * np, 512, sizeof(WfPlan)};
-    uint64_t off[10], total = 0;
-    for (int i = 0; i < 10; ++i) {
-        off[i] = total;
-        total += (sizes[i] + 255u) & ~255ull;
-    }
-    hipError_t e = hipMalloc(&s->wf_mem, total);
-    if (e != hipSuccess) {
-        s->wf_mem = nullptr;
-        return rthost::set_error(RT_ERR_OOM, std::string("hipMalloc path pool: ") + hipGetErrorString(e));
-    }
-    uint8_t* b = (uint8_t*)s->wf_mem;
-    WfPool& W = s->wp;
-    W.o = (f4*)(b + off[0]);
-    W.d = (f4*)(b + off[1]);
-    W.tl = (f4*)(b + off[2]);
-    W.lh = (f4*)(b + off[3]);
-    W.m = (uint4*)(b + off[4]);
-    W.tmax = (float*)(b + off[5]);
-    W.trace = (uint32_t*)(b + off[6]);
-    W.queue = (uint2*)(b + off[7]);
-    W.ctr = (uint32_t*)(b + off[8]);
-    W.np = np;
-    s->wf_np = np;
-    s->d_plan = (WfPlan*)(b + off[9]);
-    if ((e = hipMemcpy(s->d_plan, &s->plan, sizeof(WfPlan), hipMemcpyHostToDevice)) != hipSuccess)
-        return hip_fail(e, "upload pass plan");
-    if (!s->h_active && hipHostMalloc((void**)&s->h_active, 2 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess) {
-        s->h_active = nullptr;
-        return rthost::set_error(RT_ERR_OOM, "hipHostMalloc");
-    }
-    for (int i = 0; i < 2; ++i)
-        if (!s->round_ev[i] && (e = hipEventCreateWithFlags(&s->round_ev[i], hipEventDisableTiming)) != hipSuccess)
-            return hip_fail(e, "hipEventCreate");
-    return RT_OK;
-}
-
-// One chunk's trace stage on the wavefront path. Rounds of kRound iterations are
-// queued back to back; the host waits for round r-1's active count while round r
-// runs, and stops once a logic pass found no live path (items exhausted).
-int wf_trace(rt_scene* s, const DevCamera& cam, const DevParams& dp, const ChunkParams& q, size_t lds,
-             unsigned long long* d_segments, hipStream_t st) {
-    uint64_t total_items = (uint64_t)q.num_batches * 64u * kGroup;
-    uint32_t np_max = 4u << 20;
-    if (const char* env = getenv("RT_WF_POOL")) np_max = (uint32_t)strtoul(env, nullptr, 10);
-    if (np_max < 64u) np_max = 64u;
-    uint64_t np64 = total_items < np_max ? total_items : np_max;
-    uint32_t np = (uint32_t)((np64 + 63u) & ~63ull);
-    int rc = wf_alloc(s, np);
-    if (rc) return rc;
-    WfPool W = s->wp;
-    W.np = np;
-    hipError_t e;
-    if ((e = hipMemsetAsync(W.ctr, 0, 512, st)) != hipSuccess) return hip_fail(e, "memset counters");
-    if ((e = hipMemsetAsync(W.m, 0, 16ull * np, st)) != hipSuccess) return hip_fail(e, "memset pool");
-    if (s->grid_pass == 0) {
-        int cus = 0, a = 0, b = 0;
-        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s->device) != hipSuccess || cus < 1)
-            cus = 256;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, wf_pass, 64, lds) != hipSuccess || a < 1) a = 8;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, wf_bvh, 64, lds) != hipSuccess || b < 1) b = 8;
-        s->grid_pass = a * cus;
-        s->grid_bvh = b * cus;
-    }
-    const uint32_t kRound = 32;
-    const uint64_t max_iters = 64ull + (uint64_t)(dp.max_depth + 1u) * (total_items + np - 1u) / np * 64u;
-    uint64_t it = 0;
-    for (uint32_t round = 0;; ++round) {
-        for (uint32_t i = 0; i < kRound; ++i, ++it) {
-            uint32_t parity = (uint32_t)(it & 1u);
-            hipLaunchKernelGGL(wf_logic, dim3(np / 64u), dim3(64), lds, st, s->dev, cam, dp, q, W, s->d_plan, parity,
-                               s->sbuf, d_segments);
-            for (uint32_t p = 0; p < s->plan.npass; ++p) {
-                if (p > 0)
-                    hipLaunchKernelGGL(wf_pass, dim3((uint32_t)s->grid_pass), dim3(64), lds, st, s->dev, dp, q, W,
-                                       s->d_plan, p, parity);
-                if (s->plan.pass[p].nbvh)
-                    hipLaunchKernelGGL(wf_bvh, dim3((uint32_t)s->grid_bvh), dim3(64), lds, st, s->dev, dp, W, s->d_plan,
-                                       p, parity);
-            }
-        }
-        if ((e = hipGetLastError()) != hipSuccess) return hip_fail(e, "wavefront launch");
-        uint32_t last = (uint32_t)((it - 1u) & 1u);
-        if ((e = hipMemcpyAsync(&s->h_active[round & 1u], W.ctr + last * kCtrStride + kCtrActive, sizeof(uint32_t),
-                                hipMemcpyDeviceToHost, st)) != hipSuccess)
-            return hip_fail(e, "active count");
-        if ((e = hipEventRecord(s->round_ev[round & 1u], st)) != hipSuccess) return hip_fail(e, "round event");
-        if (round > 0) {
-            if ((e = hipEventSynchronize(s->round_ev[(round - 1u) & 1u])) != hipSuccess) return hip_fail(e, "round sync");
-            if (s->h_active[(round - 1u) & 1u] == 0u) break;
-        }
-        if (it > max_iters)
-            return rthost::set_error(RT_ERR_HIP, "wavefront trace did not drain (" + std::to_string(it) + " iterations)");
-    }
-    return RT_OK;
-}
-
-}  // namespace
 
 int rt_scene_upload(const rt_scene_desc* desc, int device, rt_scene_handle* out) {
     rthost::clear_error();
@@ -1943,7 +1399,6 @@ int rt_scene_upload(const rt_scene_desc* desc, int device, rt_scene_handle* out)
     d.num_entries = (uint32_t)hs.entries.size();
     d.stack_depth = hs.max_bvh_depth + 1u;
     s->coord_bound = hs.coord_bound;
-    s->wf = build_plan(hs, &s->plan, &s->max_pass_bvh);
     uint64_t c[10] = {hs.entries.size(), hs.sph.size(), hs.msph.size() / 3, hs.rect.size() / 2, hs.tri.size() / 3,
                       hs.nodes.size() / 2, hs.mats.size(), hs.texs.size(), hs.max_bvh_depth, total};
     memcpy(s->counts, c, sizeof c);
@@ -1966,12 +1421,22 @@ int rt_scene_free(rt_scene_handle s) {
             for (uint32_t i = 0; i < 3u * kPrCount; ++i) fprintf(stderr, "%s%llu", i ? "," : "", h[i]);
             fprintf(stderr, "]}\n");
         }
+        unsigned na = 0;
+        static LeafAudit au[kAuditMax];
+        if (hipMemcpyFromSymbol(&na, HIP_SYMBOL(g_audit_count), sizeof na) == hipSuccess &&
+            hipMemcpyFromSymbol(au, HIP_SYMBOL(g_audit), sizeof au) == hipSuccess) {
+            fprintf(stderr, "{\"leaf_audit_count\": %u}\n", na);
+            for (unsigned i = 0; i < na && i < kAuditMax; ++i)
+                fprintf(stderr,
+                        "{\"audit\": {\"o\": [%a, %a, %a], \"d\": [%a, %a, %a], \"tmin\": %a, \"closest\": %a, "
+                        "\"t\": %a, \"box\": [%a, %a, %a, %a, %a, %a], \"delta\": %a, \"code\": %u, \"rank\": %u, "
+                        "\"best_rank\": %u}}\n",
+                        au[i].o[0], au[i].o[1], au[i].o[2], au[i].d[0], au[i].d[1], au[i].d[2], au[i].tmin,
+                        au[i].closest, au[i].t, au[i].box[0], au[i].box[1], au[i].box[2], au[i].box[3], au[i].box[4],
+                        au[i].box[5], au[i].delta, au[i].code, au[i].rank, au[i].best_rank);
+        }
 #endif
         if (s->pool) (void)hipFree(s->pool);
-        if (s->wf_mem) (void)hipFree(s->wf_mem);
-        if (s->h_active) (void)hipHostFree(s->h_active);
-        for (int i = 0; i < 2; ++i)
-            if (s->round_ev[i]) (void)hipEventDestroy(s->round_ev[i]);
         if (s->sbuf) (void)hipFree(s->sbuf);
         if (s->counter) (void)hipFree(s->counter);
         for (int i = 0; i < rt_scene::kEvents; ++i)
@@ -2085,13 +1550,9 @@ int rt_render_launch(rt_scene_handle s, const rt_camera_desc* camera, const rt_r
             s->ev_overflow = true;
         }
         if (evp) (void)hipEventRecord(evp[0], st);
-        if (s->wf && (dp.tune & kModeWavefront)) {
-            if ((rc = wf_trace(s, cam, dp, q, lds, d_segments, st))) return rc;
-        } else {
-            hipLaunchKernelGGL(trace_samples, dim3(grid), dim3(64), lds, st, s->dev, cam, dp, q, s->sbuf, s->counter,
-                               d_segments);
-            if ((e = hipGetLastError()) != hipSuccess) return hip_fail(e, "trace_samples launch");
-        }
+        hipLaunchKernelGGL(trace_samples, dim3(grid), dim3(64), lds, st, s->dev, cam, dp, q, s->sbuf, s->counter,
+                           d_segments);
+        if ((e = hipGetLastError()) != hipSuccess) return hip_fail(e, "trace_samples launch");
         if (evp) {
             (void)hipEventRecord(evp[1], st);
             s->ev_count++;

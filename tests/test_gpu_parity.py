@@ -214,10 +214,13 @@ def test_c3_full_workload_subsample_matches_oracle(rt, orc):
     assert np.isfinite(got).all()
 
 
-@pytest.mark.parametrize("cfg_name,spp", [("C3", 24), ("C2", 8), ("C1", 16)])
+@pytest.mark.parametrize("cfg_name,spp", [("C3", 500), ("C2", 8), ("C1", 16)])
 def test_pruned_traversal_equals_reference_traversal_full_frame(cfg_name, spp, rt):
-    # Closest-hit box pruning must not change a single path: same bits AND the
-    # same number of ray segments as the reference's unpruned traversal.
+    # Closest-hit box pruning and leaf-box rejects must not change a single path:
+    # same bits AND the same number of ray segments as the reference's unpruned
+    # traversal. C3 runs at its full 500 spp: the rare ray parallel to a cube
+    # face through the face's plane (the reference's 0/0 = NaN rect hit) shows
+    # up a few dozen times per frame and must be traversed unpruned.
     cfg = rt.CONFIGS[cfg_name]
     cfg = cfg.scaled(cfg.width, spp)
     scene = rt.Scene.generate(cfg.scene, cfg.scene_seed)

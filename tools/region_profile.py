@@ -6,9 +6,10 @@
 
 Renders one frame with the region-instrumented build and prints, per region,
 the share of wave cycles, wave executions and the mean active lanes when the
-region ran (64 = fully converged). Regions nest: Segment contains World, Record,
-Emit, Scatter and Store; World contains the per-entry rows; Scatter contains the
-material rows; materials contain the texture rows.
+region ran (64 = fully converged). Regions nest: World contains the per-entry
+rows (and BVH trips / leaf tests); Finish segment contains Record, Emit and
+Scatter; Scatter contains the material rows; materials contain the textures.
+The library also prints leaf-box audit records (see kernel.hip LEAF_AUDIT).
 """
 import argparse
 import json
@@ -19,13 +20,10 @@ import tempfile
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-NAMES = ["Refill", "Segment", "World", "Record", "Emit", "Scatter", "Marble", "Store", "Checker", "Image",
+NAMES = ["Refill", "Finish segment", "World", "Record", "Emit", "Scatter", "Marble", "Store", "Checker", "Image",
          "UnitSphere", "Dielectric", "Lambert", "Metal", "Isotropic", "MediumLog"]
 COUNT = 48
-EXTRA = {32: "wf_logic: shade", 33: "wf_logic: regenerate", 34: "wf_logic: inline pass 0",
-         35: "wf_logic: enqueue + counters", 36: "wf_logic: whole wave", 37: "wf_pass: whole wave",
-         38: "wf_bvh: job start", 39: "wf_bvh: refill", 40: "wf_bvh: whole wave", 41: "wf: state load",
-         44: "BVH loop trip", 45: "BVH leaf test"}
+EXTRA = {44: "BVH loop trip", 45: "BVH leaf test"}
 ENTRY0 = 16
 SHOWCASE = ["boxes BVH", "light rect", "moving sphere", "glass sphere", "metal sphere", "medium boundary",
             "blue medium", "fog medium", "earth", "marble", "spheres BVH (RotY+Tr)"]
@@ -60,10 +58,14 @@ def main():
         ds.close()
         os.dup2(saved, 2)
         tf.seek(0)
-        lines = [ln for ln in tf.read().splitlines() if ln.startswith('{"rt_profile"')]
+        captured = tf.read().splitlines()
+        lines = [ln for ln in captured if ln.startswith('{"rt_profile"')]
+        for ln in captured:
+            if ln.startswith('{"leaf_audit') or ln.startswith('{"audit'):
+                print(ln)
     v = json.loads(lines[-1])["rt_profile"]
     cyc, cnt, lanes = v[:COUNT], v[COUNT:2 * COUNT], v[2 * COUNT:]
-    total = (cyc[0] + cyc[1]) or (cyc[36] + cyc[37] + cyc[40])
+    total = cyc[0] + cyc[1] + cyc[2]  # refill + finish_segment + world_hit: the whole loop
     samples = cfg.width * cfg.height * cfg.spp
     print(f"{cfg.name} {cfg.width}x{cfg.height} {cfg.spp}spp: trace {ms:.1f} ms, {segments} segments, "
           f"{segments / samples:.3f} seg/sample, wave cycles refill+segment = {total:.4g}")
