@@ -114,7 +114,7 @@ struct DevScene {
     uint32_t num_top;
     uint32_t num_entries;
     uint32_t stack_depth;  // LDS traversal stack entries per lane
-    uint32_t pad;
+    uint32_t perm_bytes;   // size of perm[] (staged in LDS when it fits)
 };
 
 // Camera::new (camera.rs:44-81) evaluated on the host.

@@ -88,8 +88,16 @@ __device__ __forceinline__ void prof_add(uint32_t region, uint64_t t0) {
 }
 #define PROF_INIT() prof_init()
 #define PROF_FLUSH() prof_flush()
-// Leaf-box audit (profiling build): leaves rejected by leaf_box_may_hit are
-// tested anyway; a rejected leaf that would have won is recorded here.
+#else
+#define PROF_T0(name) do { } while (0)
+#define PROF_ADD(region, t0) do { } while (0)
+#define PROF_INIT() do { } while (0)
+#define PROF_FLUSH() do { } while (0)
+#endif
+#ifdef RT_LEAF_AUDIT
+// Leaf-box audit (audit build, -DRT_LEAF_AUDIT -> librtamd_audit.so): leaves
+// rejected by leaf_box_may_hit are tested anyway; a rejected leaf that would have
+// produced a candidate is recorded here and printed when the scene is freed.
 struct LeafAudit {
     float o[3], d[3], tmin, closest, t, box[6], delta;
     uint32_t code, rank, best_rank;
@@ -97,11 +105,6 @@ struct LeafAudit {
 constexpr uint32_t kAuditMax = 64;
 __device__ unsigned g_audit_count;
 __device__ LeafAudit g_audit[kAuditMax];
-#else
-#define PROF_T0(name) do { } while (0)
-#define PROF_ADD(region, t0) do { } while (0)
-#define PROF_INIT() do { } while (0)
-#define PROF_FLUSH() do { } while (0)
 #endif
 
 // ---------------------------------------------------------------------------
@@ -535,8 +538,8 @@ RT_DEV bool leaf_box_may_hit(float x0, float y0, float z0, float x1, float y1, f
 // candidates provably cannot beat (closest, rank). Children are visited
 // nearest-first; ties resolve by DFS rank exactly like the recursion.
 // The stack lives in LDS, lane-strided: stack[level * 128 + {0, 64} + lane].
-#ifdef RT_PROFILE_REGIONS
-// Leaf-box audit (profiling build): a leaf rejected by leaf_box_may_hit is tested
+#ifdef RT_LEAF_AUDIT
+// Leaf-box audit (audit build): a leaf rejected by leaf_box_may_hit is tested
 // anyway, and recorded if it would have produced a candidate.
 #define LEAF_AUDIT(CODE_, RANK_, X0_, Y0_, Z0_, X1_, Y1_, Z1_)                                          \
     do {                                                                                               \
@@ -1013,6 +1016,7 @@ RT_DEV void start_sample(const DevCamera& C, const DevParams& P, const Key& k, u
 // Work items are (8x8 block, sample, pixel-in-block); a "batch" is kGroup
 // consecutive samples of one block (64 * kGroup items), blocks in shard order.
 constexpr uint32_t kGroup = 8;
+constexpr uint32_t kPermLdsMax = 4u * 9u * 256u;  // up to four Marble textures staged in LDS
 struct ChunkParams {
     uint32_t sample0;         // global sample index of chunk sample 0 (includes P.sample_base)
     uint32_t samples;         // samples per pixel in this chunk
@@ -1164,12 +1168,22 @@ RT_DEV bool finish_segment(const DevScene& S, const DevParams& P, const ChunkPar
 
 // Every live lane traces one whole segment per loop trip: the list walk with its
 // BVH traversals inline, then finish_segment.
-__global__ __launch_bounds__(64) void trace_samples(DevScene S, DevCamera C, DevParams P, ChunkParams Q,
+__global__ __launch_bounds__(64) void trace_samples(DevScene Sg, DevCamera C, DevParams P, ChunkParams Q,
                                                     float* __restrict__ sbuf, unsigned* __restrict__ batch_counter,
                                                     unsigned long long* __restrict__ seg_counter) {
     extern __shared__ uint32_t lds_stack[];
     const uint32_t lane = threadIdx.x;
     uint32_t* stk = lds_stack + lane;  // [level][{node, t_enter}][lane]
+    // Perlin permutation tables (Marble) behind the stack when they fit: the
+    // three dependent byte lookups per lattice corner then hit LDS, not L2.
+    DevScene S = Sg;
+    if (S.perm_bytes != 0u && S.perm_bytes <= kPermLdsMax) {
+        uint32_t* tab = lds_stack + S.stack_depth * 128u;
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(Sg.perm);
+        for (uint32_t i = lane; i < S.perm_bytes / 4u; i += 64u) tab[i] = src[i];
+        __syncthreads();
+        S.perm = reinterpret_cast<const uint8_t*>(tab);
+    }
     const Key k{P.seed_lo, P.seed_hi};
     const uint32_t mode = ((P.flags & RT_FLAG_EXACT_BVH) ? kModeExact : 0u) | P.tune;
     bool has = false;
@@ -1398,6 +1412,7 @@ int rt_scene_upload(const rt_scene_desc* desc, int device, rt_scene_handle* out)
     d.num_top = hs.num_top;
     d.num_entries = (uint32_t)hs.entries.size();
     d.stack_depth = hs.max_bvh_depth + 1u;
+    d.perm_bytes = (uint32_t)hs.perm.size();
     s->coord_bound = hs.coord_bound;
     uint64_t c[10] = {hs.entries.size(), hs.sph.size(), hs.msph.size() / 3, hs.rect.size() / 2, hs.tri.size() / 3,
                       hs.nodes.size() / 2, hs.mats.size(), hs.texs.size(), hs.max_bvh_depth, total};
@@ -1421,6 +1436,8 @@ int rt_scene_free(rt_scene_handle s) {
             for (uint32_t i = 0; i < 3u * kPrCount; ++i) fprintf(stderr, "%s%llu", i ? "," : "", h[i]);
             fprintf(stderr, "]}\n");
         }
+#endif
+#ifdef RT_LEAF_AUDIT
         unsigned na = 0;
         static LeafAudit au[kAuditMax];
         if (hipMemcpyFromSymbol(&na, HIP_SYMBOL(g_audit_count), sizeof na) == hipSuccess &&
@@ -1522,6 +1539,7 @@ int rt_render_launch(rt_scene_handle s, const rt_camera_desc* camera, const rt_r
             return rthost::set_error(RT_ERR_OOM, std::string("hipMalloc counter: ") + hipGetErrorString(e));
     }
     size_t lds = (size_t)s->dev.stack_depth * 128u * sizeof(uint32_t);
+    if (s->dev.perm_bytes != 0u && s->dev.perm_bytes <= kPermLdsMax) lds += s->dev.perm_bytes;
     if (s->grid == 0) {
         int per_cu = 0, cus = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace_samples, 64, lds) != hipSuccess || per_cu < 1)
