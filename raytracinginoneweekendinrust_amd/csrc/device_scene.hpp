@@ -37,6 +37,8 @@ constexpr uint32_t kLeafMedium = 6u;   // hit identifier of a ConstantMedium sca
 constexpr uint32_t kChildEmpty = 0xffffffffu;  // second child of a 1-object node (bvh.rs:261-264)
 constexpr uint32_t kMaxIndex = 0x0fffffffu;
 constexpr uint32_t kBvhPrunable = 1u;  // wrapper-node flag: closest-hit box pruning is exact for this BVH
+constexpr uint32_t kBvhWidth = 4u;     // children per BVH node (collapsed from the reference BVH2)
+constexpr uint32_t kBvhNodeF4 = 8u;    // f4 records per BVH node
 
 RTDEV_HD uint32_t leaf_code(uint32_t type, uint32_t index) {
     return kLeafBit | (type << 28) | index;
@@ -94,11 +96,13 @@ static_assert(sizeof(DevTexture) == 32, "DevTexture layout");
 //   msph : (c0, r) (c1 - c0, t0) (t1 - t0, mat, 0, 0)     moving_sphere.rs:47-51
 //   rect : (k, a0, a1, b0) (b1, axis, mat, 0)  axis 0 = XY, 1 = XZ, 2 = YZ
 //   tri  : (v0, mat) (v1 - v0, 0) (v2 - v0, 0)           triangle.rs:44-45
-//   node : 64 B BVH2 node: (Lmin, Lmax.x) (Lmax.yz, Rmin.xy) (Rmin.z, Rmax)
-//          (left, right, left rank, right rank); left/right = node index or leaf
-//          code; a leaf child has no box (tested whenever its parent is visited).
-//          Each BVH starts with a wrapper node whose only child is the root; its
-//          left-rank field holds kBvhPrunable when every leaf is a Sphere/Rect/Cube.
+//   node : 128 B BVH4 node (kBvhNodeF4 f4): (min.x[4]) (min.y[4]) (min.z[4])
+//          (max.x[4]) (max.y[4]) (max.z[4]) (child[4]) (rank[4]); child = node
+//          index, leaf code or kChildEmpty; a leaf slot's box is the leaf's own
+//          bounding box (used only by the conservative leaf reject), its rank the
+//          leaf's DFS ordinal in the reference BVH2. Each BVH starts with a wrapper
+//          node whose slot 0 is the root; the wrapper's rank[3] holds kBvhPrunable
+//          when every leaf is a Sphere/Rect/Cube.
 struct DevScene {
     const DevEntry* entries;
     const f4* sph;

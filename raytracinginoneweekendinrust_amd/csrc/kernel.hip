@@ -563,6 +563,25 @@ RT_DEV bool leaf_box_may_hit(float x0, float y0, float z0, float x1, float y1, f
 #else
 #define LEAF_AUDIT(CODE_, RANK_, X0_, Y0_, Z0_, X1_, Y1_, Z1_) do { } while (0)
 #endif
+// One interior child of a BVH4 node: the reference's box test (stored box, the
+// t_max the BVH was entered with) and, when pruning, the inflated-entry bound.
+// Returns the sort key: the entry distance, +inf when the child is not visited.
+RT_DEV float child_key(float x0, float y0, float z0, float x1, float y1, float z1, const Ray& r, V inv, float tmin,
+                       float tmax_entry, float closest, bool prune, float delta) {
+    float te;
+    bool go = slab(x0, y0, z0, x1, y1, z1, r, inv, tmin, tmax_entry, te);
+    if (go && prune) {
+        te = slab_entry_inflated(x0, y0, z0, x1, y1, z1, r, inv, tmin, delta);
+        go = !(te > prune_bound(closest));
+    }
+    return go ? (te < 3.4028235e38f ? te : 3.4028235e38f) : kInf;  // visited children sort first
+}
+RT_DEV void sort2(float& ta, uint32_t& ca, float& tb, uint32_t& cb) {
+    if (tb < ta) {
+        float t = ta; ta = tb; tb = t;
+        uint32_t c = ca; ca = cb; cb = c;
+    }
+}
 RT_DEV bool bvh_hit(const DevScene& S, float delta, uint32_t root, const Ray& r, float tmin, float& closest,
                     uint32_t& hit_code, uint32_t* stk, uint32_t mode) {
     const float tmax_entry = closest;
@@ -571,66 +590,75 @@ RT_DEV bool bvh_hit(const DevScene& S, float delta, uint32_t root, const Ray& r,
     // the plane, and every comparison against NaN passes (rectangle.rs:36-65).
     // No box bound covers that candidate, so such rays traverse unpruned.
     const bool finite_slabs = r.d.x != 0.0f && r.d.y != 0.0f && r.d.z != 0.0f;
+    const f4* wrapper = S.nodes + (size_t)root * rtdev::kBvhNodeF4;
     const bool prune = !(mode & kModeExact) && finite_slabs &&
-                       (__float_as_uint(S.nodes[4 * (size_t)root + 3].z) & rtdev::kBvhPrunable) != 0u;
+                       (__float_as_uint(wrapper[7].w) & rtdev::kBvhPrunable) != 0u;
     const bool leaf_boxes = prune && !(mode & kModeNoLeafBoxes);
     const V inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
     const RayD q = to_d(r);
     bool any = false;
     uint32_t best_rank = 0, sp = 0, cur = root;
     for (;;) {
-        const f4* nd = S.nodes + 4 * (size_t)cur;
-        f4 n0 = ld4(nd), n1 = ld4(nd + 1), n2 = ld4(nd + 2), n3 = ld4(nd + 3);
-        uint32_t lc = __float_as_uint(n3.x), rc = __float_as_uint(n3.y);
-        bool goL = false, goR = false;
-        float tl = 0.0f, tr = 0.0f;
+        const f4* nd = S.nodes + (size_t)cur * rtdev::kBvhNodeF4;
+        const f4 chf = ld4(nd + 6);
+        uint32_t c0 = __float_as_uint(chf.x), c1 = __float_as_uint(chf.y), c2 = __float_as_uint(chf.z),
+                 c3 = __float_as_uint(chf.w);
         PROF_T0(pt);
-        if (lc & rtdev::kLeafBit) {
-            if (!leaf_boxes || leaf_box_may_hit(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, r, inv, tmin, closest, delta)) {
+        // leaf slots first (the reference tests them whenever this node is
+        // visited), so the interior prune checks below see the tighter closest
+        uint32_t leaves = ((c0 & rtdev::kLeafBit) && c0 != rtdev::kChildEmpty ? 1u : 0u) |
+                          ((c1 & rtdev::kLeafBit) && c1 != rtdev::kChildEmpty ? 2u : 0u) |
+                          ((c2 & rtdev::kLeafBit) && c2 != rtdev::kChildEmpty ? 4u : 0u) |
+                          ((c3 & rtdev::kLeafBit) && c3 != rtdev::kChildEmpty ? 8u : 0u);
+        while (leaves != 0u) {
+            const uint32_t k = (uint32_t)__builtin_ctz(leaves);
+            leaves &= leaves - 1u;
+            const float* nf = reinterpret_cast<const float*>(nd);
+            const uint32_t code = __float_as_uint(nf[24 + k]), rank = __float_as_uint(nf[28 + k]);
+            const float x0 = nf[k], y0 = nf[4 + k], z0 = nf[8 + k], x1 = nf[12 + k], y1 = nf[16 + k], z1 = nf[20 + k];
+            if (!leaf_boxes || leaf_box_may_hit(x0, y0, z0, x1, y1, z1, r, inv, tmin, closest, delta)) {
                 PROF_T0(pl);
-                leaf_hit_ranked(S, lc, __float_as_uint(n3.z), r, q, tmin, closest, best_rank, hit_code, any);
+                leaf_hit_ranked(S, code, rank, r, q, tmin, closest, best_rank, hit_code, any);
                 PROF_ADD(kPrLeafTest, pl);
             } else {
-                LEAF_AUDIT(lc, __float_as_uint(n3.z), n0.x, n0.y, n0.z, n0.w, n1.x, n1.y);
-            }
-        } else {
-            goL = slab(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, r, inv, tmin, tmax_entry, tl);
-            if (goL && prune) {
-                tl = slab_entry_inflated(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, r, inv, tmin, delta);
-                goL = !(tl > prune_bound(closest));
+                LEAF_AUDIT(code, rank, x0, y0, z0, x1, y1, z1);
             }
         }
-        if (rc != rtdev::kChildEmpty) {
-            if (rc & rtdev::kLeafBit) {
-                if (!leaf_boxes ||
-                    leaf_box_may_hit(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, r, inv, tmin, closest, delta)) {
-                    PROF_T0(pl);
-                    leaf_hit_ranked(S, rc, __float_as_uint(n3.w), r, q, tmin, closest, best_rank, hit_code, any);
-                    PROF_ADD(kPrLeafTest, pl);
-                } else {
-                    LEAF_AUDIT(rc, __float_as_uint(n3.w), n1.z, n1.w, n2.x, n2.y, n2.z, n2.w);
-                }
-            } else {
-                goR = slab(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, r, inv, tmin, tmax_entry, tr);
-                if (goR && prune) {
-                    tr = slab_entry_inflated(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, r, inv, tmin, delta);
-                    goR = !(tr > prune_bound(closest));
-                }
-            }
-        }
+        // interior slots: reference box test, prune bound, nearest first
+        const f4 mnx = ld4(nd), mny = ld4(nd + 1), mnz = ld4(nd + 2), mxx = ld4(nd + 3), mxy = ld4(nd + 4),
+                 mxz = ld4(nd + 5);
+        float t0 = kInf, t1 = kInf, t2 = kInf, t3 = kInf;
+        if (!(c0 & rtdev::kLeafBit))
+            t0 = child_key(mnx.x, mny.x, mnz.x, mxx.x, mxy.x, mxz.x, r, inv, tmin, tmax_entry, closest, prune, delta);
+        if (!(c1 & rtdev::kLeafBit))
+            t1 = child_key(mnx.y, mny.y, mnz.y, mxx.y, mxy.y, mxz.y, r, inv, tmin, tmax_entry, closest, prune, delta);
+        if (!(c2 & rtdev::kLeafBit))
+            t2 = child_key(mnx.z, mny.z, mnz.z, mxx.z, mxy.z, mxz.z, r, inv, tmin, tmax_entry, closest, prune, delta);
+        if (!(c3 & rtdev::kLeafBit))
+            t3 = child_key(mnx.w, mny.w, mnz.w, mxx.w, mxy.w, mxz.w, r, inv, tmin, tmax_entry, closest, prune, delta);
         PROF_ADD(kPrBvhTrip, pt);
-        if (goL && goR) {
-            bool left_first = tl <= tr;
-            uint32_t far = left_first ? rc : lc;
-            float tfar = left_first ? tr : tl;
-            cur = left_first ? lc : rc;
-            stk[sp * 128u] = far;
-            stk[sp * 128u + 64u] = __float_as_uint(tfar);
-            sp += 1u;
-            continue;
-        }
-        if (goL || goR) {
-            cur = goL ? lc : rc;
+        sort2(t0, c0, t1, c1);
+        sort2(t2, c2, t3, c3);
+        sort2(t0, c0, t2, c2);
+        sort2(t1, c1, t3, c3);
+        sort2(t1, c1, t2, c2);
+        if (t0 != kInf) {  // visit the nearest now, push the others far to near
+            if (t3 != kInf) {
+                stk[sp * 128u] = c3;
+                stk[sp * 128u + 64u] = __float_as_uint(t3);
+                sp += 1u;
+            }
+            if (t2 != kInf) {
+                stk[sp * 128u] = c2;
+                stk[sp * 128u + 64u] = __float_as_uint(t2);
+                sp += 1u;
+            }
+            if (t1 != kInf) {
+                stk[sp * 128u] = c1;
+                stk[sp * 128u + 64u] = __float_as_uint(t1);
+                sp += 1u;
+            }
+            cur = c0;
             continue;
         }
         bool found = false;
@@ -1349,7 +1377,7 @@ int rt_scene_upload(const rt_scene_desc* desc, int device, rt_scene_handle* out)
     std::string err;
     int rc = rthost::lower_scene(desc, &hs, &err);  // validate the IR before touching a device
     if (rc) return rthost::set_error(rc, err);
-    if (hs.max_bvh_depth + 1 > 64) return rthost::set_error(RT_ERR_UNSUPPORTED, "BVH deeper than 64 levels");
+    if (hs.max_stack > 96) return rthost::set_error(RT_ERR_UNSUPPORTED, "BVH too deep for the LDS traversal stack");
     if ((rc = check_device(device))) return rc;
     struct Part {
         const void* src;
@@ -1411,11 +1439,11 @@ int rt_scene_upload(const rt_scene_desc* desc, int device, rt_scene_handle* out)
     d.texels = base + parts[10].off;
     d.num_top = hs.num_top;
     d.num_entries = (uint32_t)hs.entries.size();
-    d.stack_depth = hs.max_bvh_depth + 1u;
+    d.stack_depth = hs.max_stack;
     d.perm_bytes = (uint32_t)hs.perm.size();
     s->coord_bound = hs.coord_bound;
     uint64_t c[10] = {hs.entries.size(), hs.sph.size(), hs.msph.size() / 3, hs.rect.size() / 2, hs.tri.size() / 3,
-                      hs.nodes.size() / 2, hs.mats.size(), hs.texs.size(), hs.max_bvh_depth, total};
+                      hs.nodes.size() / rtdev::kBvhNodeF4, hs.mats.size(), hs.texs.size(), hs.max_bvh_depth, total};
     memcpy(s->counts, c, sizeof c);
     *out = s;
     return RT_OK;

@@ -563,23 +563,10 @@ class Lowerer {
             return (uint32_t)tn.size() - 1;
         };
         uint32_t troot = helper(items.data(), count, 1);
-        // Flatten to BVH2 nodes that carry both children's boxes (64 B each), in DFS
-        // preorder, behind a wrapper node whose single child is the root (so the
-        // root's box is tested on entry, as bvh.rs:370 does). Leaf children carry
-        // their DFS ordinal ("rank", cube faces rank + 0..5): the device may visit
-        // children nearest-first and still resolves equal-t ties like the
-        // reference's recursion (later in DFS order wins, bvh.rs:406-414).
-        uint32_t base = (uint32_t)(s_->nodes.size() / 4);
-        std::vector<uint32_t> remap(tn.size());
-        uint32_t next = base + 1;
-        std::function<void(uint32_t)> order = [&](uint32_t i) {
-            remap[i] = next++;
-            for (int k = 0; k < 2; ++k)
-                if (tn[i].is_node[k]) order(tn[i].child[k]);
-        };
-        order(troot);
-        if (next > rtdev::kMaxIndex) return fail(RT_ERR_UNSUPPORTED, "too many BVH nodes");
-        s_->nodes.resize((size_t)next * 4);
+        // Leaf children carry their DFS ordinal in the reference tree ("rank",
+        // cube faces rank + 0..5): the device may visit children in any order
+        // and still resolves equal-t ties like the reference's recursion (later
+        // in DFS order wins, bvh.rs:406-414).
         std::vector<uint32_t> rank(tn.size() * 2, 0);
         uint32_t ordinal = 0;
         std::function<void(uint32_t)> ranks = [&](uint32_t i) {
@@ -589,28 +576,92 @@ class Lowerer {
             }
         };
         ranks(troot);
-        auto put = [&](uint32_t o, const Box& lb, const Box& rb, uint32_t lc, uint32_t rc, uint32_t lr, uint32_t rr) {
-            s_->nodes[4 * (size_t)o + 0] = {lb.mn.x, lb.mn.y, lb.mn.z, lb.mx.x};
-            s_->nodes[4 * (size_t)o + 1] = {lb.mx.y, lb.mx.z, rb.mn.x, rb.mn.y};
-            s_->nodes[4 * (size_t)o + 2] = {rb.mn.z, rb.mx.x, rb.mx.y, rb.mx.z};
-            s_->nodes[4 * (size_t)o + 3] = {bitsf(lc), bitsf(rc), bitsf(lr), bitsf(rr)};
+        // Collapse the reference BVH2 into 4-wide nodes (rtdev::kBvhWidth). A wide
+        // node made from BVH2 node X starts with X's two children and repeatedly
+        // replaces the largest child whose own children are both interior nodes
+        // by those two children. Exactness ("BVH4 collapse"): a parent
+        // box is the min/max of its children's bounds and the slab arithmetic is
+        // monotone, so any child box passing the reference's test implies its
+        // skipped parent passes too; and a leaf still sits in the wide node made
+        // from its own BVH2 parent, whose box test is exactly the one the
+        // reference applies before testing that leaf (bvh.rs:363-417).
+        struct Slot {
+            bool node;
+            uint32_t id;  // temp node index, or leaf code
+            Box box;
+            uint32_t rank;
         };
-        const Box none{{0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f}};
-        put(base, tn[troot].box, none, remap[troot], rtdev::kChildEmpty, prunable ? rtdev::kBvhPrunable : 0u, 0u);
-        for (uint32_t i = 0; i < tn.size(); ++i) {
-            Box cb[2];
-            uint32_t cc[2];
+        auto area = [](const Box& b) {
+            float dx = b.mx.x - b.mn.x, dy = b.mx.y - b.mn.y, dz = b.mx.z - b.mn.z;
+            return dx * dy + dy * dz + dz * dx;
+        };
+        std::vector<std::vector<Slot>> wide;  // per wide node, in DFS preorder
+        std::vector<uint32_t> wide_depth;
+        std::function<uint32_t(uint32_t, uint32_t)> build4 = [&](uint32_t x, uint32_t depth) -> uint32_t {
+            std::vector<Slot> sl;
             for (int k = 0; k < 2; ++k) {
-                if (tn[i].is_node[k]) {
-                    cb[k] = tn[tn[i].child[k]].box;
-                    cc[k] = remap[tn[i].child[k]];
-                } else {
-                    cb[k] = tn[i].child[k] == rtdev::kChildEmpty ? none : tn[i].leaf_box[k];
-                    cc[k] = tn[i].child[k];
-                }
+                if (tn[x].is_node[k]) sl.push_back({true, tn[x].child[k], tn[tn[x].child[k]].box, 0u});
+                else if (tn[x].child[k] != rtdev::kChildEmpty)
+                    sl.push_back({false, tn[x].child[k], tn[x].leaf_box[k], rank[2 * x + k]});
             }
-            put(remap[i], cb[0], cb[1], cc[0], cc[1], rank[2 * i], rank[2 * i + 1]);
+            while (sl.size() < rtdev::kBvhWidth) {
+                int best = -1;
+                for (int k = 0; k < (int)sl.size(); ++k) {
+                    if (!sl[k].node) continue;
+                    const TNode& c = tn[sl[k].id];
+                    if (!(c.is_node[0] && c.is_node[1])) continue;
+                    if (best < 0 || area(sl[k].box) > area(sl[best].box)) best = k;
+                }
+                if (best < 0) break;
+                const TNode c = tn[sl[best].id];
+                sl[best] = {true, c.child[0], tn[c.child[0]].box, 0u};
+                sl.insert(sl.begin() + best + 1, Slot{true, c.child[1], tn[c.child[1]].box, 0u});
+            }
+            uint32_t me = (uint32_t)wide.size();
+            wide.push_back({});
+            wide_depth.push_back(depth);
+            for (Slot& c : sl)
+                if (c.node) c.id = build4(c.id, depth + 1) | 0x40000000u;  // mark: wide index (remapped below)
+            wide[me] = sl;
+            return me;
+        };
+        uint32_t wroot = build4(troot, 1);
+        uint32_t base = (uint32_t)(s_->nodes.size() / rtdev::kBvhNodeF4);
+        uint32_t total = base + 1 + (uint32_t)wide.size();
+        if (total > rtdev::kMaxIndex) return fail(RT_ERR_UNSUPPORTED, "too many BVH nodes");
+        s_->nodes.resize((size_t)total * rtdev::kBvhNodeF4);
+        auto put = [&](uint32_t o, const std::vector<Slot>& sl, uint32_t flags) {
+            float mnx[4], mny[4], mnz[4], mxx[4], mxy[4], mxz[4];
+            uint32_t ch[4], rk[4];
+            for (uint32_t k = 0; k < 4; ++k) {
+                const bool have = k < sl.size();
+                const Box b = have ? sl[k].box : Box{{0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f}};
+                mnx[k] = b.mn.x; mny[k] = b.mn.y; mnz[k] = b.mn.z;
+                mxx[k] = b.mx.x; mxy[k] = b.mx.y; mxz[k] = b.mx.z;
+                ch[k] = !have ? rtdev::kChildEmpty : sl[k].node ? base + 1 + (sl[k].id & ~0x40000000u) : sl[k].id;
+                rk[k] = have ? sl[k].rank : 0u;
+            }
+            rk[3] |= flags;
+            rtdev::f4* n = &s_->nodes[(size_t)o * rtdev::kBvhNodeF4];
+            n[0] = {mnx[0], mnx[1], mnx[2], mnx[3]};
+            n[1] = {mny[0], mny[1], mny[2], mny[3]};
+            n[2] = {mnz[0], mnz[1], mnz[2], mnz[3]};
+            n[3] = {mxx[0], mxx[1], mxx[2], mxx[3]};
+            n[4] = {mxy[0], mxy[1], mxy[2], mxy[3]};
+            n[5] = {mxz[0], mxz[1], mxz[2], mxz[3]};
+            n[6] = {bitsf(ch[0]), bitsf(ch[1]), bitsf(ch[2]), bitsf(ch[3])};
+            n[7] = {bitsf(rk[0]), bitsf(rk[1]), bitsf(rk[2]), bitsf(rk[3])};
+        };
+        // wrapper: slot 0 = the root (its box is tested on entry, bvh.rs:370);
+        // its rank[3] carries the BVH's flags
+        put(base, {Slot{true, wroot | 0x40000000u, tn[troot].box, 0u}}, prunable ? rtdev::kBvhPrunable : 0u);
+        uint32_t max_wide_depth = 0;
+        for (uint32_t w = 0; w < wide.size(); ++w) {
+            put(base + 1 + w, wide[w], 0u);
+            max_wide_depth = std::max(max_wide_depth, wide_depth[w]);
         }
+        // a visit pushes at most kBvhWidth - 1 siblings per level
+        s_->max_stack = std::max(s_->max_stack, (rtdev::kBvhWidth - 1u) * max_wide_depth + 1u);
         s_->max_bvh_depth = std::max(s_->max_bvh_depth, max_depth_ + 1);
         *root_out = base;
         return RT_OK;

@@ -21,7 +21,8 @@ struct HostScene {
     std::vector<rtdev::DevMaterial> mats;
     std::vector<rtdev::DevTexture> texs;
     std::vector<uint8_t> perm, texels;
-    uint32_t max_bvh_depth = 0;  // internal levels of the deepest BVH
+    uint32_t max_bvh_depth = 0;  // internal levels of the deepest BVH (reference BVH2)
+    uint32_t max_stack = 1;      // traversal stack entries per lane (BVH4)
     // Upper bound on |coordinate| of any primitive in any instance frame plus the
     // translations applied to reach it (bounds ray lengths for the pruning margin).
     float coord_bound = 0.0f;
