@@ -102,7 +102,9 @@ static_assert(sizeof(DevTexture) == 32, "DevTexture layout");
 //          bounding box (used only by the conservative leaf reject), its rank the
 //          leaf's DFS ordinal in the reference BVH2. Each BVH starts with a wrapper
 //          node whose slot 0 is the root; the wrapper's rank[3] holds kBvhPrunable
-//          when every leaf is a Sphere/Rect/Cube.
+//          when every leaf is a Sphere/Rect/Cube, its rank[2] the BVH2 wrapper.
+//   node2: 64 B reference BVH2 node: (Lmin, Lmax.x) (Lmax.yz, Rmin.xy) (Rmin.z,
+//          Rmax) (left, right, 0, 0), DFS preorder behind a wrapper (child 0 = root).
 struct DevScene {
     const DevEntry* entries;
     const f4* sph;
@@ -111,6 +113,7 @@ struct DevScene {
     const f4* rect;
     const f4* tri;
     const f4* nodes;
+    const f4* nodes2;  // the reference BVH2 trees (bvh_hit_reference)
     const DevMaterial* mats;
     const DevTexture* texs;
     const uint8_t* perm;

@@ -105,6 +105,13 @@ struct LeafAudit {
 constexpr uint32_t kAuditMax = 64;
 __device__ unsigned g_audit_count;
 __device__ LeafAudit g_audit[kAuditMax];
+// and every fast traversal is replayed with bvh_hit_reference; disagreements land here
+struct TravAudit {
+    float o[3], d[3], tmin, tmax, fast_t, ref_t;
+    uint32_t fast_code, ref_code, root;
+};
+__device__ unsigned g_trav_audit_count;
+__device__ TravAudit g_trav_audit[kAuditMax];
 #endif
 
 // ---------------------------------------------------------------------------
@@ -445,38 +452,6 @@ RT_DEV bool slab(float x0, float y0, float z0, float x1, float y1, float z1, con
     return !(t_max < t_min);
 }
 
-// A BVH leaf inside the traversal: candidates must beat (closest, best_rank)
-// lexicographically — smaller t, or equal t and later in the reference's DFS order.
-RT_DEV void leaf_hit_ranked(const DevScene& S, uint32_t code, uint32_t rank, const Ray& r, const RayD& q, float tmin,
-                            float& closest, uint32_t& best_rank, uint32_t& hit_code, bool& any) {
-    uint32_t type = rtdev::leaf_type(code), idx = rtdev::leaf_index(code);
-    float t;
-    if (type == rtdev::kLeafCube) {  // cube.rs:84-93: six sides, later faces win ties
-        for (uint32_t i = 0; i < 6u; ++i) {
-            uint32_t ri = idx + i;
-            if (rect_t(ld4(S.rect + 2 * ri), ld4(S.rect + 2 * ri + 1), r, tmin, closest, t) &&
-                (t < closest || rank + i > best_rank)) {
-                closest = t;
-                best_rank = rank + i;
-                hit_code = rtdev::leaf_code(rtdev::kLeafRect, ri);
-                any = true;
-            }
-        }
-        return;
-    }
-    bool h;
-    if (type == rtdev::kLeafSphere) h = sphere_t(ld4(S.sph + idx), q, tmin, closest, t);
-    else if (type == rtdev::kLeafTri) h = tri_t(ld4(S.tri + 3 * idx), ld4(S.tri + 3 * idx + 1), ld4(S.tri + 3 * idx + 2), r, tmin, closest, t);
-    else if (type == rtdev::kLeafRect) h = rect_t(ld4(S.rect + 2 * idx), ld4(S.rect + 2 * idx + 1), r, tmin, closest, t);
-    else h = msphere_t(ld4(S.msph + 3 * idx), ld4(S.msph + 3 * idx + 1), ld4(S.msph + 3 * idx + 2), r, tmin, closest, t);
-    if (h && (t < closest || rank > best_rank)) {
-        closest = t;
-        best_rank = rank;
-        hit_code = code;
-        any = true;
-    }
-}
-
 // Entry parameter of the ray into a box inflated by `delta` on every side (the
 // near-side half of the slab test above, on outward-rounded bounds).
 RT_DEV float slab_entry_inflated(float x0, float y0, float z0, float x1, float y1, float z1, const Ray& r, V inv,
@@ -543,11 +518,9 @@ RT_DEV bool leaf_box_may_hit(float x0, float y0, float z0, float x1, float y1, f
 // anyway, and recorded if it would have produced a candidate.
 #define LEAF_AUDIT(CODE_, RANK_, X0_, Y0_, Z0_, X1_, Y1_, Z1_)                                          \
     do {                                                                                               \
-        float c_ = closest;                                                                            \
-        uint32_t br_ = best_rank, hc_ = 0u;                                                            \
-        bool any_ = false;                                                                             \
-        leaf_hit_ranked(S, (CODE_), (RANK_), r, q, tmin, c_, br_, hc_, any_);                          \
-        if (any_) {                                                                                    \
+        float c_ = tmax_entry;                                                                         \
+        uint32_t hc_ = 0u;                                                                             \
+        if (leaf_hit(S, (CODE_), r, q, tmin, c_, hc_) && !(c_ > bound)) {                              \
             unsigned i_ = atomicAdd(&g_audit_count, 1u);                                               \
             if (i_ < kAuditMax) {                                                                      \
                 LeafAudit& A = g_audit[i_];                                                            \
@@ -556,13 +529,128 @@ RT_DEV bool leaf_box_may_hit(float x0, float y0, float z0, float x1, float y1, f
                 A.tmin = tmin; A.closest = closest; A.t = c_; A.delta = delta;                         \
                 A.box[0] = (X0_); A.box[1] = (Y0_); A.box[2] = (Z0_);                                  \
                 A.box[3] = (X1_); A.box[4] = (Y1_); A.box[5] = (Z1_);                                  \
-                A.code = (CODE_); A.rank = (RANK_); A.best_rank = best_rank;                           \
+                A.code = (CODE_); A.rank = (RANK_); A.best_rank = hc_;                                 \
             }                                                                                          \
         }                                                                                              \
     } while (0)
 #else
 #define LEAF_AUDIT(CODE_, RANK_, X0_, Y0_, Z0_, X1_, Y1_, Z1_) do { } while (0)
 #endif
+// BvhNode::hit (bvh.rs:363-417) replayed literally on the reference BVH2: the
+// node's box with the BVH's entry t_max, the left child (an Index child with
+// t_max, a Hittable with t_max), then the right child (an Index child with
+// t_max, a Hittable with the left hit's t), and `if left.t < right.t {left}
+// else {right}`. The reference kernel (trace_samples<true>) traverses every BVH
+// this way: RT_FLAG_EXACT_BVH renders, and the samples the fast kernel hands
+// over because one of their rays could take a NaN hit (with a NaN t in play the
+// tree-min is neither associative nor order-independent, so only the
+// reference's own recursion order is exact).
+// One frame per level: stk[level * 256 + {0, 64, 128, 192} + lane] = node,
+// phase | left-hit << 2, left t, left code. Phases: 0 start, 1 waiting for the
+// left subtree, 2 left known, 3 waiting for the right subtree.
+RT_DEV bool bvh_hit_reference(const DevScene& S, uint32_t wrapper2, const Ray& r, const RayD& q, V inv, float tmin,
+                              float& closest, uint32_t& hit_code, uint32_t* stk) {
+    const float tmax = closest;
+    const f4* w = S.nodes2 + 4 * (size_t)wrapper2;
+    {
+        f4 w0 = ld4(w), w1 = ld4(w + 1);
+        float te;
+        if (!slab(w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, r, inv, tmin, tmax, te)) return false;  // bvh.rs:370
+    }
+    uint32_t sp = 1u;
+    stk[0] = __float_as_uint(ld4(w + 3).x);
+    stk[64] = 0u;
+    bool rh = false, returning = false;
+    float rt = 0.0f;
+    uint32_t rcode = 0u;
+    for (;;) {
+        uint32_t* F = stk + (sp - 1u) * 256u;
+        uint32_t st = F[64];
+        if (returning) {  // deliver the finished child's result to its parent frame
+            if ((st & 3u) == 1u) {
+                F[64] = 2u | (rh ? 4u : 0u);
+                F[128] = __float_as_uint(rt);
+                F[192] = rcode;
+                returning = false;
+                continue;
+            }
+            // phase 3: right subtree done -> combine with the stored left result
+            if ((st & 4u) && !(rh && !(__uint_as_float(F[128]) < rt))) {
+                rt = __uint_as_float(F[128]);
+                rcode = F[192];
+                rh = true;
+            }
+            sp -= 1u;
+            if (sp == 0u) break;
+            continue;
+        }
+        const f4* nd = S.nodes2 + 4 * (size_t)F[0];
+        f4 n0 = ld4(nd), n1 = ld4(nd + 1), n2 = ld4(nd + 2), n3 = ld4(nd + 3);
+        const uint32_t lc = __float_as_uint(n3.x), rc = __float_as_uint(n3.y);
+        if ((st & 3u) == 0u) {  // left child
+            if (lc & rtdev::kLeafBit) {
+                float c = tmax;
+                uint32_t code = 0u;
+                bool h = leaf_hit(S, lc, r, q, tmin, c, code);
+                F[64] = 2u | (h ? 4u : 0u);
+                F[128] = __float_as_uint(c);
+                F[192] = code;
+            } else {
+                float te;
+                if (slab(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, r, inv, tmin, tmax, te)) {
+                    F[64] = 1u;
+                    stk[sp * 256u] = lc;
+                    stk[sp * 256u + 64u] = 0u;
+                    sp += 1u;
+                } else {
+                    F[64] = 2u;
+                }
+            }
+            continue;
+        }
+        // phase 2: right child (a 1-object node repeats its left object: same result)
+        const bool hl = (st & 4u) != 0u;
+        const float tl = __uint_as_float(F[128]);
+        if (rc == rtdev::kChildEmpty || (rc & rtdev::kLeafBit)) {
+            float c = hl ? tl : tmax;  // t_max_for_right
+            uint32_t code = 0u;
+            bool hr = rc != rtdev::kChildEmpty && leaf_hit(S, rc, r, q, tmin, c, code);
+            if (hr && !(hl && tl < c)) {
+                rh = true;
+                rt = c;
+                rcode = code;
+            } else {
+                rh = hl;
+                rt = tl;
+                rcode = F[192];
+            }
+            sp -= 1u;
+            if (sp == 0u) break;
+            returning = true;
+            continue;
+        }
+        float te;
+        if (slab(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, r, inv, tmin, tmax, te)) {
+            F[64] = 3u | (st & 4u);
+            stk[sp * 256u] = rc;
+            stk[sp * 256u + 64u] = 0u;
+            sp += 1u;
+        } else {  // no right hit: the left result stands
+            rh = hl;
+            rt = tl;
+            rcode = F[192];
+            sp -= 1u;
+            if (sp == 0u) break;
+            returning = true;
+        }
+    }
+    if (rh) {
+        closest = rt;
+        hit_code = rcode;
+    }
+    return rh;
+}
+
 // One interior child of a BVH4 node: the reference's box test (stored box, the
 // t_max the BVH was entered with) and, when pruning, the inflated-entry bound.
 // Returns the sort key: the entry distance, +inf when the child is not visited.
@@ -582,20 +670,27 @@ RT_DEV void sort2(float& ta, uint32_t& ca, float& tb, uint32_t& cb) {
         uint32_t c = ca; ca = cb; cb = c;
     }
 }
+// kRef: the reference kernel replays bvh.rs literally. The fast kernel
+// returns with `replay` set for a ray that could take a NaN hit: a ray parallel
+// to an axis plane (a zero direction component) gets t = (k - o) / d = 0 / 0 from
+// a rect whose plane holds its origin, and every comparison against NaN passes
+// (rectangle.rs:36-65); its sample is re-traced by the reference kernel.
+template <bool kRef>
 RT_DEV bool bvh_hit(const DevScene& S, float delta, uint32_t root, const Ray& r, float tmin, float& closest,
-                    uint32_t& hit_code, uint32_t* stk, uint32_t mode) {
+                    uint32_t& hit_code, uint32_t* stk, uint32_t mode, bool& replay) {
     const float tmax_entry = closest;
-    // A ray parallel to an axis plane (a zero direction component) can take the
-    // reference's NaN rect hit: t = (k - o) / d = 0 / 0 when the origin lies on
-    // the plane, and every comparison against NaN passes (rectangle.rs:36-65).
-    // No box bound covers that candidate, so such rays traverse unpruned.
-    const bool finite_slabs = r.d.x != 0.0f && r.d.y != 0.0f && r.d.z != 0.0f;
     const f4* wrapper = S.nodes + (size_t)root * rtdev::kBvhNodeF4;
-    const bool prune = !(mode & kModeExact) && finite_slabs &&
-                       (__float_as_uint(wrapper[7].w) & rtdev::kBvhPrunable) != 0u;
-    const bool leaf_boxes = prune && !(mode & kModeNoLeafBoxes);
     const V inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
     const RayD q = to_d(r);
+    if constexpr (kRef) {
+        return bvh_hit_reference(S, __float_as_uint(wrapper[7].z), r, q, inv, tmin, closest, hit_code, stk);
+    }
+    if (r.d.x == 0.0f || r.d.y == 0.0f || r.d.z == 0.0f) {
+        replay = true;
+        return false;
+    }
+    const bool prune = (__float_as_uint(wrapper[7].w) & rtdev::kBvhPrunable) != 0u;
+    const bool leaf_boxes = prune && !(mode & kModeNoLeafBoxes);
     bool any = false;
     uint32_t best_rank = 0, sp = 0, cur = root;
     for (;;) {
@@ -604,25 +699,63 @@ RT_DEV bool bvh_hit(const DevScene& S, float delta, uint32_t root, const Ray& r,
         uint32_t c0 = __float_as_uint(chf.x), c1 = __float_as_uint(chf.y), c2 = __float_as_uint(chf.z),
                  c3 = __float_as_uint(chf.w);
         PROF_T0(pt);
-        // leaf slots first (the reference tests them whenever this node is
-        // visited), so the interior prune checks below see the tighter closest
+        // Leaf slots first, so the interior prune checks below see the tighter
+        // closest. They are the leaf children of ONE reference BVH2 node, left
+        // then right (bvh.rs never mixes leaf and Index children), and that node's
+        // result is formed exactly like bvh.rs:377-414: the left leaf is tested
+        // with the BVH's entry t_max, the right one with the left hit's t
+        // (t_max_for_right), and `if left.t < right.t {left} else {right}`. This
+        // matters for f64 spheres: sphere.rs compares its root against the f32
+        // t_max before rounding t to f32, so a sphere whose rounded t equals
+        // another candidate's passes or fails depending on which t_max it saw.
+        // The node result then joins (closest, DFS rank) like the tree-min does.
         uint32_t leaves = ((c0 & rtdev::kLeafBit) && c0 != rtdev::kChildEmpty ? 1u : 0u) |
                           ((c1 & rtdev::kLeafBit) && c1 != rtdev::kChildEmpty ? 2u : 0u) |
                           ((c2 & rtdev::kLeafBit) && c2 != rtdev::kChildEmpty ? 4u : 0u) |
                           ((c3 & rtdev::kLeafBit) && c3 != rtdev::kChildEmpty ? 8u : 0u);
+        float tmr = tmax_entry, nt = 0.0f;
+        bool nh = false;
+        uint32_t ncode = 0u, nrank = 0u;
         while (leaves != 0u) {
             const uint32_t k = (uint32_t)__builtin_ctz(leaves);
             leaves &= leaves - 1u;
             const float* nf = reinterpret_cast<const float*>(nd);
-            const uint32_t code = __float_as_uint(nf[24 + k]), rank = __float_as_uint(nf[28 + k]);
+            const uint32_t lcode = __float_as_uint(nf[24 + k]), rank = __float_as_uint(nf[28 + k]);
             const float x0 = nf[k], y0 = nf[4 + k], z0 = nf[8 + k], x1 = nf[12 + k], y1 = nf[16 + k], z1 = nf[20 + k];
-            if (!leaf_boxes || leaf_box_may_hit(x0, y0, z0, x1, y1, z1, r, inv, tmin, closest, delta)) {
+            // the right leaf can only matter if t <= min(closest, left t)
+            const float bound = tmr < closest ? tmr : closest;
+            if (!leaf_boxes || leaf_box_may_hit(x0, y0, z0, x1, y1, z1, r, inv, tmin, bound, delta)) {
                 PROF_T0(pl);
-                leaf_hit_ranked(S, code, rank, r, q, tmin, closest, best_rank, hit_code, any);
+                // Only candidates whose f32 t can tie or beat closest matter, so
+                // the test may use min(t_max, nextup(closest)): a root in
+                // (closest, nextup] is still judged against the reference's own
+                // t_max, anything beyond rounds above closest and loses anyway.
+                const float cap = closest < kInf ? __uint_as_float(__float_as_uint(closest) + 1u) : kInf;
+                float c = tmr < cap ? tmr : cap;
+                uint32_t code = 0u;
+                if (leaf_hit(S, lcode, r, q, tmin, c, code)) {
+                    // cube faces rank + 0..5 (the face leaf_hit's list walk kept)
+                    const uint32_t rk = rank + (rtdev::leaf_type(lcode) == rtdev::kLeafCube
+                                                    ? rtdev::leaf_index(code) - rtdev::leaf_index(lcode)
+                                                    : 0u);
+                    if (!nh || !(nt < c)) {
+                        nh = true;
+                        nt = c;
+                        ncode = code;
+                        nrank = rk;
+                    }
+                    tmr = c;
+                }
                 PROF_ADD(kPrLeafTest, pl);
             } else {
-                LEAF_AUDIT(code, rank, x0, y0, z0, x1, y1, z1);
+                LEAF_AUDIT(lcode, rank, x0, y0, z0, x1, y1, z1);
             }
+        }
+        if (nh && (nt < closest || (nt == closest && nrank > best_rank))) {
+            closest = nt;
+            best_rank = nrank;
+            hit_code = ncode;
+            any = true;
         }
         // interior slots: reference box test, prune bound, nearest first
         const f4 mnx = ld4(nd), mny = ld4(nd + 1), mnz = ld4(nd + 2), mxx = ld4(nd + 3), mxy = ld4(nd + 4),
@@ -674,6 +807,26 @@ RT_DEV bool bvh_hit(const DevScene& S, float delta, uint32_t root, const Ray& r,
         }
         if (!found) break;
     }
+#ifdef RT_LEAF_AUDIT
+    {  // the replay of the reference recursion must agree with the fast traversal
+        float c2 = tmax_entry;
+        uint32_t h2 = 0u;
+        bool a2 = bvh_hit_reference(S, __float_as_uint(wrapper[7].z), r, q, inv, tmin, c2, h2, stk);
+        bool same = a2 == any && (!any || (__float_as_uint(c2) == __float_as_uint(closest) && h2 == hit_code));
+        if (!same) {
+            unsigned i_ = atomicAdd(&g_trav_audit_count, 1u);
+            if (i_ < kAuditMax) {
+                TravAudit& A = g_trav_audit[i_];
+                A.o[0] = r.o.x; A.o[1] = r.o.y; A.o[2] = r.o.z;
+                A.d[0] = r.d.x; A.d[1] = r.d.y; A.d[2] = r.d.z;
+                A.tmin = tmin; A.tmax = tmax_entry;
+                A.fast_t = any ? closest : kInf; A.ref_t = a2 ? c2 : kInf;
+                A.fast_code = any ? hit_code : 0xffffffffu; A.ref_code = a2 ? h2 : 0xffffffffu;
+                A.root = root;
+            }
+        }
+    }
+#endif
     return any;
 }
 
@@ -690,19 +843,22 @@ RT_DEV Ray apply_op(f4 op, Ray r) {
 }
 
 // A GEOM or BVH entry (the caller guarantees E is wave-uniform).
+template <bool kRef>
 RT_DEV bool entry_geom_hit(const DevScene& S, float delta, const DevEntry* E, Ray r, float tmin, float& closest,
-                           uint32_t& hit_code, uint32_t* stk, uint32_t exact) {
+                           uint32_t& hit_code, uint32_t* stk, uint32_t mode, bool& replay) {
     uint32_t ntf = E->ntf;
     for (uint32_t i = 0; i < ntf; ++i) r = apply_op(E->tf[i], r);
-    if (E->kind == rtdev::kEntBvh) return bvh_hit(S, delta, E->payload, r, tmin, closest, hit_code, stk, exact);
+    if (E->kind == rtdev::kEntBvh)
+        return bvh_hit<kRef>(S, delta, E->payload, r, tmin, closest, hit_code, stk, mode, replay);
     RayD q = to_d(r);
     return leaf_hit(S, E->payload, r, q, tmin, closest, hit_code);
 }
 
 // ConstantMedium::hit (hittable.rs:176-233); draws one U(0,1) once the clamped
 // interval is non-empty, exactly where the reference does.
+template <bool kRef>
 RT_DEV bool medium_hit(const DevScene& S, float delta, const DevEntry* E, Ray r, float tmin, float tmax, Rng& g,
-                       const Key& k, float& t_out, uint32_t* stk, uint32_t exact) {
+                       const Key& k, float& t_out, uint32_t* stk, uint32_t mode, bool& replay) {
     uint32_t ntf = E->ntf;
     for (uint32_t i = 0; i < ntf; ++i) r = apply_op(E->tf[i], r);
     const DevEntry* B = S.entries + E->payload;
@@ -718,8 +874,8 @@ RT_DEV bool medium_hit(const DevScene& S, float delta, const DevEntry* E, Ray r,
         if (!sphere_select(R, t1 + 0.0001f, kInf, t2)) return false;
     } else {
         uint32_t dummy;
-        if (!entry_geom_hit(S, delta, B, r, -kInf, t1, dummy, stk, exact)) return false;
-        if (!entry_geom_hit(S, delta, B, r, t1 + 0.0001f, t2, dummy, stk, exact)) return false;
+        if (!entry_geom_hit<kRef>(S, delta, B, r, -kInf, t1, dummy, stk, mode, replay)) return false;
+        if (!entry_geom_hit<kRef>(S, delta, B, r, t1 + 0.0001f, t2, dummy, stk, mode, replay)) return false;
     }
     if (t1 < tmin) t1 = tmin;
     if (t2 > tmax) t2 = tmax;
@@ -1054,8 +1210,9 @@ struct ChunkParams {
 };
 
 // HittableList::hit over the world (hittable.rs:100-118), t in [0.001, inf).
+template <bool kRef>
 RT_DEV bool world_hit(const DevScene& S, float delta, const Ray& r, Rng& g, const Key& k, float& t_hit,
-                      uint32_t& hit_entry, uint32_t& hit_code, uint32_t* stk, uint32_t mode) {
+                      uint32_t& hit_entry, uint32_t& hit_code, uint32_t* stk, uint32_t mode, bool& replay) {
     float closest = kInf;
     bool any = false;
     for (uint32_t e = 0; e < S.num_top; ++e) {
@@ -1063,7 +1220,7 @@ RT_DEV bool world_hit(const DevScene& S, float delta, const Ray& r, Rng& g, cons
         PROF_T0(pe);
         if (E->kind == rtdev::kEntMedium) {
             float t;
-            if (medium_hit(S, delta, E, r, 0.001f, closest, g, k, t, stk, mode)) {
+            if (medium_hit<kRef>(S, delta, E, r, 0.001f, closest, g, k, t, stk, mode, replay)) {
                 closest = t;
                 hit_entry = e;
                 hit_code = rtdev::leaf_code(rtdev::kLeafMedium, 0);
@@ -1071,7 +1228,7 @@ RT_DEV bool world_hit(const DevScene& S, float delta, const Ray& r, Rng& g, cons
             }
         } else {
             uint32_t code;
-            if (entry_geom_hit(S, delta, E, r, 0.001f, closest, code, stk, mode)) {
+            if (entry_geom_hit<kRef>(S, delta, E, r, 0.001f, closest, code, stk, mode, replay)) {
                 hit_entry = e;
                 hit_code = code;
                 any = true;
@@ -1094,40 +1251,64 @@ struct ItemPool {  // wave-uniform
     uint32_t batch, next, end;
     bool exhausted;
 };
+// Per-chunk device counters of the trace stage (zeroed before each chunk).
+struct TraceCounters {
+    unsigned batch;              // next 8x8-block batch of the fast (or exact) kernel
+    unsigned replay_count;       // samples handed to the reference kernel
+    unsigned replay_pull;        // next replay-list entry (reference kernel)
+    unsigned batch_full;         // next batch when the replay list overflowed
+    unsigned long long fast_segments;  // segments of the fast kernel's completed samples
+};
+// A replay-list entry: the sample's pixel and its chunk-local sample index.
+struct ReplayItem {
+    uint32_t pixel, sample;
+};
 // Gives the next work item to every lane with `want` set. A lane that got a
 // sample returns true with its camera ray started (renderer.rs:141-143); a
 // max_depth 0 sample (ray.rs:39-41: black, no segment) is stored and skipped.
+// With `list` set, the items are that many replay-list entries instead (pulled
+// 64 at a time through *counter).
 RT_DEV bool take_sample(ItemPool& pool, bool want, const DevCamera& C, const DevParams& P, const ChunkParams& Q,
-                        const Key& k, unsigned* batch_counter, float* sbuf, uint32_t lane, uint32_t& pixel,
-                        uint32_t& s_local, V& L, V& T, uint32_t& depth, Rng& g, Ray& ray) {
+                        const Key& k, unsigned* counter, const ReplayItem* list, uint32_t list_n, float* sbuf,
+                        uint32_t lane, uint32_t& pixel, uint32_t& s_local, V& L, V& T, uint32_t& depth, Rng& g,
+                        Ray& ray) {
     bool got = false;
     for (;;) {
         unsigned long long need = __ballot(want && !got);
         if (need == 0ull || pool.exhausted) break;
         if (pool.next == pool.end) {
             uint32_t bt = 0;
-            if (lane == 0u) bt = atomicAdd(batch_counter, 1u);
+            if (lane == 0u) bt = atomicAdd(counter, list ? 64u : 1u);
             bt = __builtin_amdgcn_readfirstlane(bt);
-            if (bt >= Q.num_batches) {
+            if (bt >= (list ? list_n : Q.num_batches)) {
                 pool.exhausted = true;
                 break;
             }
             pool.batch = bt;
-            pool.next = 0u;
-            pool.end = 64u * kGroup;
+            pool.next = list ? bt : 0u;
+            pool.end = list ? (bt + 64u < list_n ? bt + 64u : list_n) : 64u * kGroup;
             continue;
         }
         uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
         uint32_t avail = pool.end - pool.next;
         if (want && !got && rank < avail) {
-            uint32_t item = pool.next + rank;
-            uint32_t blk_local = pool.batch / Q.groups_per_block;
-            uint32_t grp = pool.batch - blk_local * Q.groups_per_block;
-            uint32_t s = grp * kGroup + (item >> 6);
-            uint32_t pib = item & 63u;
-            uint32_t blk = P.shard_index + blk_local * P.shard_count;
-            uint32_t by = blk / P.blocks_x, bx = blk - by * P.blocks_x;
-            uint32_t x = bx * 8u + (pib & 7u), y = by * 8u + (pib >> 3);
+            uint32_t x, y, s;
+            if (list) {
+                const ReplayItem it = list[pool.next + rank];
+                y = it.pixel / P.width;
+                x = it.pixel - y * P.width;
+                s = it.sample;
+            } else {
+                uint32_t item = pool.next + rank;
+                uint32_t blk_local = pool.batch / Q.groups_per_block;
+                uint32_t grp = pool.batch - blk_local * Q.groups_per_block;
+                s = grp * kGroup + (item >> 6);
+                uint32_t pib = item & 63u;
+                uint32_t blk = P.shard_index + blk_local * P.shard_count;
+                uint32_t by = blk / P.blocks_x, bx = blk - by * P.blocks_x;
+                x = bx * 8u + (pib & 7u);
+                y = by * 8u + (pib >> 3);
+            }
             if (x < P.width && y < P.height && s < Q.samples) {
                 pixel = y * P.width + x;
                 s_local = s;
@@ -1196,8 +1377,22 @@ RT_DEV bool finish_segment(const DevScene& S, const DevParams& P, const ChunkPar
 
 // Every live lane traces one whole segment per loop trip: the list walk with its
 // BVH traversals inline, then finish_segment.
+//
+// trace_samples<false> is the fast kernel (BVH4, nearest-first, exact pruning).
+// A sample whose ray could take a NaN hit in a BVH is handed to the reference
+// kernel instead: it is dropped here (its partial segments uncounted) and listed
+// in `replay`. trace_samples<true> traverses every BVH with the literal replay
+// of bvh.rs; it renders whole chunks under RT_FLAG_EXACT_BVH (fixup == 0) and
+// otherwise re-traces the listed samples from their camera ray (fixup == 1).
+// Samples are independent and keyed by (pixel, global sample index), so the
+// re-traced sample is exactly the reference's. Should the list overflow, the
+// fixup kernel re-renders the whole chunk and takes back the fast kernel's
+// segment count.
+constexpr uint32_t kReplayCap = 1u << 20;
+template <bool kRef>
 __global__ __launch_bounds__(64) void trace_samples(DevScene Sg, DevCamera C, DevParams P, ChunkParams Q,
-                                                    float* __restrict__ sbuf, unsigned* __restrict__ batch_counter,
+                                                    float* __restrict__ sbuf, TraceCounters* __restrict__ ctr,
+                                                    ReplayItem* __restrict__ replay_list, uint32_t fixup,
                                                     unsigned long long* __restrict__ seg_counter) {
     extern __shared__ uint32_t lds_stack[];
     const uint32_t lane = threadIdx.x;
@@ -1213,9 +1408,28 @@ __global__ __launch_bounds__(64) void trace_samples(DevScene Sg, DevCamera C, De
         S.perm = reinterpret_cast<const uint8_t*>(tab);
     }
     const Key k{P.seed_lo, P.seed_hi};
-    const uint32_t mode = ((P.flags & RT_FLAG_EXACT_BVH) ? kModeExact : 0u) | P.tune;
+    const uint32_t mode = P.tune;
+    // item source: the chunk's block batches, or (fixup) the replay list
+    unsigned* counter = &ctr->batch;
+    const ReplayItem* list = nullptr;
+    uint32_t list_n = 0u;
+    if (kRef && fixup) {
+        const uint32_t n = __hip_atomic_load(&ctr->replay_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (n <= kReplayCap) {
+            if (n == 0u) return;
+            list = replay_list;
+            list_n = n;
+            counter = &ctr->replay_pull;
+        } else {  // overflow: re-render the chunk; its segments replace the fast kernel's
+            counter = &ctr->batch_full;
+            if (blockIdx.x == 0u && lane == 0u && seg_counter)
+                atomicAdd(seg_counter, 0ull - __hip_atomic_load(&ctr->fast_segments, __ATOMIC_RELAXED,
+                                                                __HIP_MEMORY_SCOPE_AGENT));
+        }
+    }
     bool has = false;
-    uint32_t pixel = 0, s_local = 0, depth = 0, nseg = 0;
+    uint32_t pixel = 0, s_local = 0, depth = 0;
+    unsigned long long nseg = 0, nseg_sample = 0;
     V L = mk(0.0f, 0.0f, 0.0f), T = mk(1.0f, 1.0f, 1.0f);
     Rng g{};
     Ray ray{};
@@ -1223,24 +1437,38 @@ __global__ __launch_bounds__(64) void trace_samples(DevScene Sg, DevCamera C, De
     PROF_INIT();
     for (;;) {
         PROF_T0(pr);
-        if (take_sample(pool, !has, C, P, Q, k, batch_counter, sbuf, lane, pixel, s_local, L, T, depth, g, ray))
+        if (take_sample(pool, !has, C, P, Q, k, counter, list, list_n, sbuf, lane, pixel, s_local, L, T, depth, g,
+                        ray)) {
             has = true;
+            nseg_sample = 0;
+        }
         PROF_ADD(kPrRefill, pr);
         if (__ballot(has) == 0ull) break;  // pool exhausted and every path finished
         if (has) {
-            nseg += 1u;
+            nseg_sample += 1u;
             float t;
             uint32_t he = 0, hc = 0;
+            bool replay = false;
             PROF_T0(pw);
-            bool any = world_hit(S, P.prune_delta, ray, g, k, t, he, hc, stk, mode);
+            bool any = world_hit<kRef>(S, P.prune_delta, ray, g, k, t, he, hc, stk, mode, replay);
             PROF_ADD(kPrWorld, pw);
-            if (finish_segment(S, P, Q, k, sbuf, any, he, hc, t, ray, L, T, depth, g, pixel, s_local)) has = false;
+            if (!kRef && replay) {  // hand the sample to the reference kernel
+                unsigned idx = atomicAdd(&ctr->replay_count, 1u);
+                if (idx < kReplayCap) replay_list[idx] = ReplayItem{pixel, s_local};
+                has = false;
+            } else if (finish_segment(S, P, Q, k, sbuf, any, he, hc, t, ray, L, T, depth, g, pixel, s_local)) {
+                has = false;
+                nseg += nseg_sample;
+            }
         }
     }
     if (seg_counter) {
         unsigned long long v = nseg;
         for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-        if (lane == 0u) atomicAdd(seg_counter, v);
+        if (lane == 0u) {
+            atomicAdd(seg_counter, v);
+            if (!kRef) atomicAdd(&ctr->fast_segments, v);
+        }
     }
     PROF_FLUSH();
 }
@@ -1299,12 +1527,14 @@ struct rt_scene {
     uint64_t pool_bytes = 0;
     DevScene dev{};
     uint64_t counts[10] = {};
-    // render workspace (sample buffer + batch counter), grown on demand; one render
+    // render workspace (sample buffer, counters, replay list), grown on demand; one render
     // at a time per scene handle
     float* sbuf = nullptr;
     uint64_t sbuf_bytes = 0;
-    unsigned* counter = nullptr;
-    int grid = 0;  // resident waves of trace_samples
+    TraceCounters* counter = nullptr;
+    uint32_t stack_ref = 1;  // LDS stack entries per lane of trace_samples<true> (dev.stack_depth: <false>)
+    int grid = 0, grid_ref = 0;  // resident waves of trace_samples<false> / <true>
+    ReplayItem* replay = nullptr;  // kReplayCap entries
     float coord_bound = 0.0f;
     // HIP events bracketing every trace launch (rt_scene_trace_time)
     static constexpr int kEvents = 256;
@@ -1377,7 +1607,8 @@ int rt_scene_upload(const rt_scene_desc* desc, int device, rt_scene_handle* out)
     std::string err;
     int rc = rthost::lower_scene(desc, &hs, &err);  // validate the IR before touching a device
     if (rc) return rthost::set_error(rc, err);
-    if (hs.max_stack > 96) return rthost::set_error(RT_ERR_UNSUPPORTED, "BVH too deep for the LDS traversal stack");
+    if (hs.max_stack > 96 || hs.max_stack_ref > 96)
+        return rthost::set_error(RT_ERR_UNSUPPORTED, "BVH too deep for the LDS traversal stack");
     if ((rc = check_device(device))) return rc;
     struct Part {
         const void* src;
@@ -1396,6 +1627,7 @@ int rt_scene_upload(const rt_scene_desc* desc, int device, rt_scene_handle* out)
         {hs.texs.data(), hs.texs.size() * sizeof(DevTexture), 0},
         {hs.perm.data(), hs.perm.size(), 0},
         {hs.texels.data(), hs.texels.size(), 0},
+        {hs.nodes2.data(), hs.nodes2.size() * sizeof(f4), 0},
     };
     uint64_t total = 0;
     for (auto& p : parts) {
@@ -1437,9 +1669,11 @@ int rt_scene_upload(const rt_scene_desc* desc, int device, rt_scene_handle* out)
     d.texs = (const DevTexture*)(base + parts[8].off);
     d.perm = base + parts[9].off;
     d.texels = base + parts[10].off;
+    d.nodes2 = (const f4*)(base + parts[11].off);
     d.num_top = hs.num_top;
     d.num_entries = (uint32_t)hs.entries.size();
     d.stack_depth = hs.max_stack;
+    s->stack_ref = hs.max_stack_ref;
     d.perm_bytes = (uint32_t)hs.perm.size();
     s->coord_bound = hs.coord_bound;
     uint64_t c[10] = {hs.entries.size(), hs.sph.size(), hs.msph.size() / 3, hs.rect.size() / 2, hs.tri.size() / 3,
@@ -1480,10 +1714,22 @@ int rt_scene_free(rt_scene_handle s) {
                         au[i].closest, au[i].t, au[i].box[0], au[i].box[1], au[i].box[2], au[i].box[3], au[i].box[4],
                         au[i].box[5], au[i].delta, au[i].code, au[i].rank, au[i].best_rank);
         }
+        static TravAudit ta[kAuditMax];
+        if (hipMemcpyFromSymbol(&na, HIP_SYMBOL(g_trav_audit_count), sizeof na) == hipSuccess &&
+            hipMemcpyFromSymbol(ta, HIP_SYMBOL(g_trav_audit), sizeof ta) == hipSuccess) {
+            fprintf(stderr, "{\"trav_audit_count\": %u}\n", na);
+            for (unsigned i = 0; i < na && i < kAuditMax; ++i)
+                fprintf(stderr,
+                        "{\"trav_audit\": {\"o\": [%a, %a, %a], \"d\": [%a, %a, %a], \"tmin\": %a, \"tmax\": %a, "
+                        "\"fast_t\": %a, \"ref_t\": %a, \"fast_code\": %u, \"ref_code\": %u, \"root\": %u}}\n",
+                        ta[i].o[0], ta[i].o[1], ta[i].o[2], ta[i].d[0], ta[i].d[1], ta[i].d[2], ta[i].tmin, ta[i].tmax,
+                        ta[i].fast_t, ta[i].ref_t, ta[i].fast_code, ta[i].ref_code, ta[i].root);
+        }
 #endif
         if (s->pool) (void)hipFree(s->pool);
         if (s->sbuf) (void)hipFree(s->sbuf);
         if (s->counter) (void)hipFree(s->counter);
+        if (s->replay) (void)hipFree(s->replay);
         for (int i = 0; i < rt_scene::kEvents; ++i)
             for (int j = 0; j < 2; ++j)
                 if (s->ev[i][j]) (void)hipEventDestroy(s->ev[i][j]);
@@ -1563,19 +1809,33 @@ int rt_render_launch(rt_scene_handle s, const rt_camera_desc* camera, const rt_r
         s->sbuf_bytes = need;
     }
     if (!s->counter) {
-        if ((e = hipMalloc(&s->counter, 256)) != hipSuccess)
+        if ((e = hipMalloc(&s->counter, sizeof(TraceCounters))) != hipSuccess)
             return rthost::set_error(RT_ERR_OOM, std::string("hipMalloc counter: ") + hipGetErrorString(e));
     }
-    size_t lds = (size_t)s->dev.stack_depth * 128u * sizeof(uint32_t);
-    if (s->dev.perm_bytes != 0u && s->dev.perm_bytes <= kPermLdsMax) lds += s->dev.perm_bytes;
+    if (!s->replay) {
+        if ((e = hipMalloc(&s->replay, sizeof(ReplayItem) * (size_t)kReplayCap)) != hipSuccess)
+            return rthost::set_error(RT_ERR_OOM, std::string("hipMalloc replay list: ") + hipGetErrorString(e));
+    }
+    // LDS per wave: the kernel's traversal stack, then the Perlin tables
+    DevScene dev_ref = s->dev;
+    dev_ref.stack_depth = s->stack_ref;
+    const size_t perm_lds = s->dev.perm_bytes != 0u && s->dev.perm_bytes <= kPermLdsMax ? s->dev.perm_bytes : 0u;
+    const size_t lds = (size_t)s->dev.stack_depth * 128u * sizeof(uint32_t) + perm_lds;
+    const size_t lds_ref = (size_t)dev_ref.stack_depth * 128u * sizeof(uint32_t) + perm_lds;
     if (s->grid == 0) {
-        int per_cu = 0, cus = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace_samples, 64, lds) != hipSuccess || per_cu < 1)
+        int per_cu = 0, per_cu_ref = 0, cus = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace_samples<false>, 64, lds) != hipSuccess ||
+            per_cu < 1)
             per_cu = 8;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_ref, trace_samples<true>, 64, lds_ref) != hipSuccess ||
+            per_cu_ref < 1)
+            per_cu_ref = 8;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s->device) != hipSuccess || cus < 1)
             cus = 256;
         s->grid = per_cu * cus;
+        s->grid_ref = per_cu_ref * cus;
     }
+    const bool exact = (dp.flags & RT_FLAG_EXACT_BVH) != 0u;
     hipStream_t st = (hipStream_t)stream;
     for (uint32_t c = 0; c < nchunks; ++c) {
         ChunkParams q;
@@ -1584,9 +1844,11 @@ int rt_render_launch(rt_scene_handle s, const rt_camera_desc* camera, const rt_r
         q.groups_per_block = (q.samples + kGroup - 1) / kGroup;
         q.num_batches = nblk * q.groups_per_block;
         q.npix = (uint32_t)npix;
-        if ((e = hipMemsetAsync(s->counter, 0, sizeof(unsigned), st)) != hipSuccess) return hip_fail(e, "memset counter");
-        uint32_t grid = (uint32_t)s->grid;
+        if ((e = hipMemsetAsync(s->counter, 0, sizeof(TraceCounters), st)) != hipSuccess)
+            return hip_fail(e, "memset counters");
+        uint32_t grid = (uint32_t)s->grid, grid_ref = (uint32_t)s->grid_ref;
         if (grid > q.num_batches) grid = q.num_batches;
+        if (grid_ref > q.num_batches) grid_ref = q.num_batches;
         hipEvent_t* evp = nullptr;
         if (s->ev_count < rt_scene::kEvents) {
             evp = s->ev[s->ev_count];
@@ -1596,8 +1858,15 @@ int rt_render_launch(rt_scene_handle s, const rt_camera_desc* camera, const rt_r
             s->ev_overflow = true;
         }
         if (evp) (void)hipEventRecord(evp[0], st);
-        hipLaunchKernelGGL(trace_samples, dim3(grid), dim3(64), lds, st, s->dev, cam, dp, q, s->sbuf, s->counter,
-                           d_segments);
+        if (exact) {  // every BVH traversed by the literal replay of bvh.rs
+            hipLaunchKernelGGL(trace_samples<true>, dim3(grid_ref), dim3(64), lds_ref, st, dev_ref, cam, dp, q,
+                               s->sbuf, s->counter, s->replay, 0u, d_segments);
+        } else {  // fast kernel, then the reference kernel on the samples it handed over
+            hipLaunchKernelGGL(trace_samples<false>, dim3(grid), dim3(64), lds, st, s->dev, cam, dp, q, s->sbuf,
+                               s->counter, s->replay, 0u, d_segments);
+            hipLaunchKernelGGL(trace_samples<true>, dim3(grid_ref), dim3(64), lds_ref, st, dev_ref, cam, dp, q,
+                               s->sbuf, s->counter, s->replay, 1u, d_segments);
+        }
         if ((e = hipGetLastError()) != hipSuccess) return hip_fail(e, "trace_samples launch");
         if (evp) {
             (void)hipEventRecord(evp[1], st);

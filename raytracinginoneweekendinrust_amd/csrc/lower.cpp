@@ -28,7 +28,7 @@ using rtdev::f4;
 
 uint64_t HostScene::bytes() const {
     return entries.size() * sizeof(rtdev::DevEntry) + sph.size() * 16 + sph_mat.size() * 4 +
-           msph.size() * 16 + rect.size() * 16 + tri.size() * 16 + nodes.size() * 16 +
+           msph.size() * 16 + rect.size() * 16 + tri.size() * 16 + nodes.size() * 16 + nodes2.size() * 16 +
            mats.size() * sizeof(rtdev::DevMaterial) + texs.size() * sizeof(rtdev::DevTexture) +
            perm.size() + texels.size();
 }
@@ -626,6 +626,38 @@ class Lowerer {
             return me;
         };
         uint32_t wroot = build4(troot, 1);
+        // The reference tree itself, as 64 B BVH2 nodes (both children's boxes,
+        // child codes), DFS preorder behind a wrapper whose child 0 is the root:
+        // traversed in the reference's own recursion order by rays that can take
+        // a NaN hit, and by every ray under RT_FLAG_EXACT_BVH (bvh_hit_reference).
+        const uint32_t base2 = (uint32_t)(s_->nodes2.size() / 4);
+        std::vector<uint32_t> remap2(tn.size());
+        uint32_t next2 = base2 + 1;
+        std::function<void(uint32_t)> order2 = [&](uint32_t i) {
+            remap2[i] = next2++;
+            for (int k = 0; k < 2; ++k)
+                if (tn[i].is_node[k]) order2(tn[i].child[k]);
+        };
+        order2(troot);
+        if (next2 > rtdev::kMaxIndex) return fail(RT_ERR_UNSUPPORTED, "too many BVH nodes");
+        s_->nodes2.resize((size_t)next2 * 4);
+        auto put2 = [&](uint32_t o, const Box& lb, const Box& rb, uint32_t lc, uint32_t rc) {
+            s_->nodes2[4 * (size_t)o + 0] = {lb.mn.x, lb.mn.y, lb.mn.z, lb.mx.x};
+            s_->nodes2[4 * (size_t)o + 1] = {lb.mx.y, lb.mx.z, rb.mn.x, rb.mn.y};
+            s_->nodes2[4 * (size_t)o + 2] = {rb.mn.z, rb.mx.x, rb.mx.y, rb.mx.z};
+            s_->nodes2[4 * (size_t)o + 3] = {bitsf(lc), bitsf(rc), 0.0f, 0.0f};
+        };
+        const Box none2{{0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f}};
+        put2(base2, tn[troot].box, none2, remap2[troot], rtdev::kChildEmpty);
+        for (uint32_t i = 0; i < tn.size(); ++i) {
+            Box cb[2];
+            uint32_t cc[2];
+            for (int k = 0; k < 2; ++k) {
+                cb[k] = tn[i].is_node[k] ? tn[tn[i].child[k]].box : none2;
+                cc[k] = tn[i].is_node[k] ? remap2[tn[i].child[k]] : tn[i].child[k];
+            }
+            put2(remap2[i], cb[0], cb[1], cc[0], cc[1]);
+        }
         uint32_t base = (uint32_t)(s_->nodes.size() / rtdev::kBvhNodeF4);
         uint32_t total = base + 1 + (uint32_t)wide.size();
         if (total > rtdev::kMaxIndex) return fail(RT_ERR_UNSUPPORTED, "too many BVH nodes");
@@ -655,13 +687,16 @@ class Lowerer {
         // wrapper: slot 0 = the root (its box is tested on entry, bvh.rs:370);
         // its rank[3] carries the BVH's flags
         put(base, {Slot{true, wroot | 0x40000000u, tn[troot].box, 0u}}, prunable ? rtdev::kBvhPrunable : 0u);
+        s_->nodes[(size_t)base * rtdev::kBvhNodeF4 + 7].z = bitsf(base2);  // wrapper rank[2]: the BVH2 wrapper
         uint32_t max_wide_depth = 0;
         for (uint32_t w = 0; w < wide.size(); ++w) {
             put(base + 1 + w, wide[w], 0u);
             max_wide_depth = std::max(max_wide_depth, wide_depth[w]);
         }
-        // a visit pushes at most kBvhWidth - 1 siblings per level
+        // a BVH4 visit pushes at most kBvhWidth - 1 siblings per level (2 words
+        // each); the BVH2 recursion (reference kernel) keeps one 4-word frame per level
         s_->max_stack = std::max(s_->max_stack, (rtdev::kBvhWidth - 1u) * max_wide_depth + 1u);
+        s_->max_stack_ref = std::max(s_->max_stack_ref, 2u * (max_depth_ + 2u));
         s_->max_bvh_depth = std::max(s_->max_bvh_depth, max_depth_ + 1);
         *root_out = base;
         return RT_OK;

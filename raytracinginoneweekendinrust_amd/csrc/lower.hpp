@@ -17,12 +17,13 @@ struct HostScene {
     uint32_t num_top = 0;
     std::vector<rtdev::f4> sph;
     std::vector<uint32_t> sph_mat;
-    std::vector<rtdev::f4> msph, rect, tri, nodes;
+    std::vector<rtdev::f4> msph, rect, tri, nodes, nodes2;
     std::vector<rtdev::DevMaterial> mats;
     std::vector<rtdev::DevTexture> texs;
     std::vector<uint8_t> perm, texels;
     uint32_t max_bvh_depth = 0;  // internal levels of the deepest BVH (reference BVH2)
-    uint32_t max_stack = 1;      // traversal stack entries per lane (BVH4)
+    uint32_t max_stack = 1;      // BVH4 traversal stack entries (2 words) per lane
+    uint32_t max_stack_ref = 1;  // the same for the BVH2 replay (reference kernel)
     // Upper bound on |coordinate| of any primitive in any instance frame plus the
     // translations applied to reach it (bounds ray lengths for the pruning margin).
     float coord_bound = 0.0f;

@@ -34,8 +34,8 @@ def main():
     ap.add_argument("--config", default="C3")
     ap.add_argument("--spp", type=int, default=None)
     args = ap.parse_args()
-    if "prof" not in os.environ.get("RT_LIBRARY", ""):
-        sys.exit("set RT_LIBRARY to the _prof build")
+    if not any(k in os.environ.get("RT_LIBRARY", "") for k in ("_prof", "_audit")):
+        sys.exit("set RT_LIBRARY to the _prof or _audit build")
     import torch
     import raytracinginoneweekendinrust_amd as rt
     cfg = rt.CONFIGS[args.config]
@@ -61,8 +61,10 @@ def main():
         captured = tf.read().splitlines()
         lines = [ln for ln in captured if ln.startswith('{"rt_profile"')]
         for ln in captured:
-            if ln.startswith('{"leaf_audit') or ln.startswith('{"audit'):
+            if ln.startswith(('{"leaf_audit', '{"audit', '{"trav_audit')):
                 print(ln)
+    if not lines:  # an audit build: no region counters
+        return
     v = json.loads(lines[-1])["rt_profile"]
     cyc, cnt, lanes = v[:COUNT], v[COUNT:2 * COUNT], v[2 * COUNT:]
     total = cyc[0] + cyc[1] + cyc[2]  # refill + finish_segment + world_hit: the whole loop
