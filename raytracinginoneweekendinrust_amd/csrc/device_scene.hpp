@@ -39,6 +39,11 @@ constexpr uint32_t kMaxIndex = 0x0fffffffu;
 constexpr uint32_t kBvhPrunable = 1u;  // wrapper-node flag: closest-hit box pruning is exact for this BVH
 constexpr uint32_t kBvhWidth = 4u;     // children per BVH node (collapsed from the reference BVH2)
 constexpr uint32_t kBvhNodeF4 = 8u;    // f4 records per BVH node
+// A BVH4 node holds either only leaves (the 1-2 leaf children of one reference
+// BVH2 node, in slots 0-1) or only interior children (bvh.rs never mixes them);
+// child pointers to a leaf node carry this bit so the traversal knows which rows
+// to load before loading anything.
+constexpr uint32_t kLeafNodeFlag = 0x40000000u;
 
 RTDEV_HD uint32_t leaf_code(uint32_t type, uint32_t index) {
     return kLeafBit | (type << 28) | index;
@@ -98,7 +103,7 @@ static_assert(sizeof(DevTexture) == 32, "DevTexture layout");
 //   tri  : (v0, mat) (v1 - v0, 0) (v2 - v0, 0)           triangle.rs:44-45
 //   node : 128 B BVH4 node (kBvhNodeF4 f4): (min.x[4]) (min.y[4]) (min.z[4])
 //          (max.x[4]) (max.y[4]) (max.z[4]) (child[4]) (rank[4]); child = node
-//          index, leaf code or kChildEmpty; a leaf slot's box is the leaf's own
+//          index (| kLeafNodeFlag for a leaf node), leaf code or kChildEmpty; a leaf slot's box is the leaf's own
 //          bounding box (used only by the conservative leaf reject), its rank the
 //          leaf's DFS ordinal in the reference BVH2. Each BVH starts with a wrapper
 //          node whose slot 0 is the root; the wrapper's rank[3] holds kBvhPrunable

@@ -58,21 +58,28 @@ constexpr float kInf = __builtin_inff();
 enum ProfRegion : uint32_t {
     kPrRefill = 0, kPrSegment, kPrWorld, kPrRecord, kPrEmit, kPrScatter, kPrMarble, kPrStore,
     kPrChecker, kPrImage, kPrUnitSphere, kPrDielectric, kPrLambert, kPrMetal, kPrIso, kPrLog,
-    kPrEntry0 = 16, kPrEntryLast = 43, kPrBvhTrip = 44, kPrLeafTest = 45, kPrCount = 48
+    kPrEntry0 = 16, kPrEntryLast = 43, kPrBvhTrip = 44, kPrLeafTest = 45, kPrBvhSetup = 46, kPrBvhPush = 47,
+    kPrBvhPop = 48, kPrBvhCall = 49, kPrCount = 52
 };
 // traversal mode bits (bvh_hit): kModeExact = RT_FLAG_EXACT_BVH; the rest come
 // from DevParams::tune (RT_TUNE environment variable, diagnostics / A-B runs).
 constexpr uint32_t kModeExact = 1u, kModeNoLeafBoxes = 2u;
 #ifdef RT_PROFILE_REGIONS
 constexpr uint32_t kProfCopies = 64;  // flush targets spread over blockIdx to keep atomics uncontended
-__device__ unsigned long long g_prof[kProfCopies * 3 * kPrCount];
-__shared__ unsigned long long prof_lds[3 * kPrCount];
+constexpr uint32_t kProfWords = 3 * kPrCount + 16;  // region triples, then the two visit histograms
+__device__ unsigned long long g_prof[kProfCopies * kProfWords];
+__shared__ unsigned long long prof_lds[kProfWords];
+// per-traversal node-visit histograms (prof_lds[3 * kPrCount + bin]: lanes,
+// [3 * kPrCount + 8 + bin]: the wave's max per call); bins 0,1,2,3-4,5-8,9-16,17-32,33+
+__device__ __forceinline__ uint32_t trips_bin(uint32_t n) {
+    return n == 0u ? 0u : n == 1u ? 1u : n == 2u ? 2u : n <= 4u ? 3u : n <= 8u ? 4u : n <= 16u ? 5u : n <= 32u ? 6u : 7u;
+}
 __device__ __forceinline__ void prof_init() {
-    for (uint32_t i = threadIdx.x; i < 3u * kPrCount; i += blockDim.x) prof_lds[i] = 0u;
+    for (uint32_t i = threadIdx.x; i < kProfWords; i += blockDim.x) prof_lds[i] = 0u;
 }
 __device__ __forceinline__ void prof_flush() {
-    unsigned long long* dst = g_prof + (blockIdx.x % kProfCopies) * 3u * kPrCount;
-    for (uint32_t i = threadIdx.x; i < 3u * kPrCount; i += blockDim.x)
+    unsigned long long* dst = g_prof + (blockIdx.x % kProfCopies) * kProfWords;
+    for (uint32_t i = threadIdx.x; i < kProfWords; i += blockDim.x)
         if (prof_lds[i]) atomicAdd(&dst[i], prof_lds[i]);
 }
 #define PROF_T0(name) const uint64_t name = __builtin_amdgcn_s_memtime()
@@ -147,6 +154,9 @@ RT_DEV float rs_clamp(float x, float lo, float hi) {
 RT_DEV bool sign_negative(float x) { return (__float_as_uint(x) >> 31) != 0u; }
 RT_DEV bool sign_negative_d(double x) { return (__double_as_longlong(x) >> 63) != 0; }
 RT_DEV V xyz(f4 a) { return V{a.x, a.y, a.z}; }
+RT_DEV float2 ld2(const f4* p, uint32_t row) {  // the .xy half of row `row`
+    return *reinterpret_cast<const float2*>(p + row);
+}
 RT_DEV f4 ld4(const f4* p) {
     float4 v = *reinterpret_cast<const float4*>(p);
     return f4{v.x, v.y, v.z, v.w};
@@ -678,6 +688,8 @@ RT_DEV void sort2(float& ta, uint32_t& ca, float& tb, uint32_t& cb) {
 template <bool kRef>
 RT_DEV bool bvh_hit(const DevScene& S, float delta, uint32_t root, const Ray& r, float tmin, float& closest,
                     uint32_t& hit_code, uint32_t* stk, uint32_t mode, bool& replay) {
+    PROF_T0(pcall);
+    PROF_T0(psetup);
     const float tmax_entry = closest;
     const f4* wrapper = S.nodes + (size_t)root * rtdev::kBvhNodeF4;
     const V inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
@@ -693,83 +705,100 @@ RT_DEV bool bvh_hit(const DevScene& S, float delta, uint32_t root, const Ray& r,
     const bool leaf_boxes = prune && !(mode & kModeNoLeafBoxes);
     bool any = false;
     uint32_t best_rank = 0, sp = 0, cur = root;
+    PROF_ADD(kPrBvhSetup, psetup);
+#ifdef RT_PROFILE_REGIONS
+    uint32_t visits = 0;
+#endif
     for (;;) {
-        const f4* nd = S.nodes + (size_t)cur * rtdev::kBvhNodeF4;
-        const f4 chf = ld4(nd + 6);
-        uint32_t c0 = __float_as_uint(chf.x), c1 = __float_as_uint(chf.y), c2 = __float_as_uint(chf.z),
-                 c3 = __float_as_uint(chf.w);
+        // One batch of loads per step: a leaf node needs the .xy halves of its
+        // rows, an interior node its six box rows and child codes.
+        const bool leaf_node = (cur & rtdev::kLeafNodeFlag) != 0u;
+        const f4* nd = S.nodes + (size_t)(cur & ~rtdev::kLeafNodeFlag) * rtdev::kBvhNodeF4;
+#ifdef RT_PROFILE_REGIONS
+        ++visits;
+#endif
         PROF_T0(pt);
-        // Leaf slots first, so the interior prune checks below see the tighter
-        // closest. They are the leaf children of ONE reference BVH2 node, left
-        // then right (bvh.rs never mixes leaf and Index children), and that node's
-        // result is formed exactly like bvh.rs:377-414: the left leaf is tested
-        // with the BVH's entry t_max, the right one with the left hit's t
-        // (t_max_for_right), and `if left.t < right.t {left} else {right}`. This
-        // matters for f64 spheres: sphere.rs compares its root against the f32
-        // t_max before rounding t to f32, so a sphere whose rounded t equals
-        // another candidate's passes or fails depending on which t_max it saw.
-        // The node result then joins (closest, DFS rank) like the tree-min does.
-        uint32_t leaves = ((c0 & rtdev::kLeafBit) && c0 != rtdev::kChildEmpty ? 1u : 0u) |
-                          ((c1 & rtdev::kLeafBit) && c1 != rtdev::kChildEmpty ? 2u : 0u) |
-                          ((c2 & rtdev::kLeafBit) && c2 != rtdev::kChildEmpty ? 4u : 0u) |
-                          ((c3 & rtdev::kLeafBit) && c3 != rtdev::kChildEmpty ? 8u : 0u);
-        float tmr = tmax_entry, nt = 0.0f;
-        bool nh = false;
-        uint32_t ncode = 0u, nrank = 0u;
-        while (leaves != 0u) {
-            const uint32_t k = (uint32_t)__builtin_ctz(leaves);
-            leaves &= leaves - 1u;
-            const float* nf = reinterpret_cast<const float*>(nd);
-            const uint32_t lcode = __float_as_uint(nf[24 + k]), rank = __float_as_uint(nf[28 + k]);
-            const float x0 = nf[k], y0 = nf[4 + k], z0 = nf[8 + k], x1 = nf[12 + k], y1 = nf[16 + k], z1 = nf[20 + k];
-            // the right leaf can only matter if t <= min(closest, left t)
-            const float bound = tmr < closest ? tmr : closest;
-            if (!leaf_boxes || leaf_box_may_hit(x0, y0, z0, x1, y1, z1, r, inv, tmin, bound, delta)) {
-                PROF_T0(pl);
-                // Only candidates whose f32 t can tie or beat closest matter, so
-                // the test may use min(t_max, nextup(closest)): a root in
-                // (closest, nextup] is still judged against the reference's own
-                // t_max, anything beyond rounds above closest and loses anyway.
-                const float cap = closest < kInf ? __uint_as_float(__float_as_uint(closest) + 1u) : kInf;
-                float c = tmr < cap ? tmr : cap;
-                uint32_t code = 0u;
-                if (leaf_hit(S, lcode, r, q, tmin, c, code)) {
-                    // cube faces rank + 0..5 (the face leaf_hit's list walk kept)
-                    const uint32_t rk = rank + (rtdev::leaf_type(lcode) == rtdev::kLeafCube
-                                                    ? rtdev::leaf_index(code) - rtdev::leaf_index(lcode)
-                                                    : 0u);
-                    if (!nh || !(nt < c)) {
-                        nh = true;
-                        nt = c;
-                        ncode = code;
-                        nrank = rk;
+        if (leaf_node) {
+            // The 1-2 leaf children of ONE reference BVH2 node, left then right,
+            // and that node's result formed exactly like bvh.rs:377-414: the left
+            // leaf is tested with the BVH's entry t_max, the right one with the
+            // left hit's t (t_max_for_right), and `if left.t < right.t {left} else
+            // {right}`. This matters for f64 spheres: sphere.rs compares its root
+            // against the f32 t_max before rounding t to f32, so a sphere whose
+            // rounded t equals another candidate's passes or fails depending on
+            // which t_max it saw. The node result then joins (closest, DFS rank)
+            // like the tree-min does.
+            const float2 bx0 = ld2(nd, 0), by0 = ld2(nd, 1), bz0 = ld2(nd, 2), bx1 = ld2(nd, 3), by1 = ld2(nd, 4),
+                         bz1 = ld2(nd, 5), chs = ld2(nd, 6), rks = ld2(nd, 7);
+            float tmr = tmax_entry, nt = 0.0f;
+            bool nh = false;
+            uint32_t ncode = 0u, nrank = 0u;
+            const uint32_t nleaf = __float_as_uint(chs.y) == rtdev::kChildEmpty ? 1u : 2u;
+            for (uint32_t k = 0; k < nleaf; ++k) {
+                const uint32_t lcode = __float_as_uint(k ? chs.y : chs.x), rank = __float_as_uint(k ? rks.y : rks.x);
+                const float x0 = k ? bx0.y : bx0.x, y0 = k ? by0.y : by0.x, z0 = k ? bz0.y : bz0.x;
+                const float x1 = k ? bx1.y : bx1.x, y1 = k ? by1.y : by1.x, z1 = k ? bz1.y : bz1.x;
+                // the right leaf can only matter if t <= min(closest, left t)
+                const float bound = tmr < closest ? tmr : closest;
+                if (!leaf_boxes || leaf_box_may_hit(x0, y0, z0, x1, y1, z1, r, inv, tmin, bound, delta)) {
+                    PROF_T0(pl);
+                    // Only candidates whose f32 t can tie or beat closest matter, so
+                    // the test may use min(t_max, nextup(closest)): a root in
+                    // (closest, nextup] is still judged against the reference's own
+                    // t_max, anything beyond rounds above closest and loses anyway.
+                    const float cap = closest < kInf ? __uint_as_float(__float_as_uint(closest) + 1u) : kInf;
+                    float c = tmr < cap ? tmr : cap;
+                    uint32_t code = 0u;
+                    if (leaf_hit(S, lcode, r, q, tmin, c, code)) {
+                        // cube faces rank + 0..5 (the face leaf_hit's list walk kept)
+                        const uint32_t rk = rank + (rtdev::leaf_type(lcode) == rtdev::kLeafCube
+                                                        ? rtdev::leaf_index(code) - rtdev::leaf_index(lcode)
+                                                        : 0u);
+                        if (!nh || !(nt < c)) {
+                            nh = true;
+                            nt = c;
+                            ncode = code;
+                            nrank = rk;
+                        }
+                        tmr = c;
                     }
-                    tmr = c;
+                    PROF_ADD(kPrLeafTest, pl);
+                } else {
+                    LEAF_AUDIT(lcode, rank, x0, y0, z0, x1, y1, z1);
                 }
-                PROF_ADD(kPrLeafTest, pl);
-            } else {
-                LEAF_AUDIT(lcode, rank, x0, y0, z0, x1, y1, z1);
+            }
+            if (nh && (nt < closest || (nt == closest && nrank > best_rank))) {
+                closest = nt;
+                best_rank = nrank;
+                hit_code = ncode;
+                any = true;
             }
         }
-        if (nh && (nt < closest || (nt == closest && nrank > best_rank))) {
-            closest = nt;
-            best_rank = nrank;
-            hit_code = ncode;
-            any = true;
-        }
-        // interior slots: reference box test, prune bound, nearest first
-        const f4 mnx = ld4(nd), mny = ld4(nd + 1), mnz = ld4(nd + 2), mxx = ld4(nd + 3), mxy = ld4(nd + 4),
-                 mxz = ld4(nd + 5);
         float t0 = kInf, t1 = kInf, t2 = kInf, t3 = kInf;
-        if (!(c0 & rtdev::kLeafBit))
-            t0 = child_key(mnx.x, mny.x, mnz.x, mxx.x, mxy.x, mxz.x, r, inv, tmin, tmax_entry, closest, prune, delta);
-        if (!(c1 & rtdev::kLeafBit))
-            t1 = child_key(mnx.y, mny.y, mnz.y, mxx.y, mxy.y, mxz.y, r, inv, tmin, tmax_entry, closest, prune, delta);
-        if (!(c2 & rtdev::kLeafBit))
-            t2 = child_key(mnx.z, mny.z, mnz.z, mxx.z, mxy.z, mxz.z, r, inv, tmin, tmax_entry, closest, prune, delta);
-        if (!(c3 & rtdev::kLeafBit))
-            t3 = child_key(mnx.w, mny.w, mnz.w, mxx.w, mxy.w, mxz.w, r, inv, tmin, tmax_entry, closest, prune, delta);
+        uint32_t c0 = rtdev::kChildEmpty, c1 = rtdev::kChildEmpty, c2 = rtdev::kChildEmpty, c3 = rtdev::kChildEmpty;
+        if (!leaf_node) {
+            // interior slots: reference box test, prune bound, nearest first
+            const f4 mnx = ld4(nd), mny = ld4(nd + 1), mnz = ld4(nd + 2), mxx = ld4(nd + 3), mxy = ld4(nd + 4),
+                     mxz = ld4(nd + 5), chf = ld4(nd + 6);
+            c0 = __float_as_uint(chf.x);
+            c1 = __float_as_uint(chf.y);
+            c2 = __float_as_uint(chf.z);
+            c3 = __float_as_uint(chf.w);
+            if (c0 != rtdev::kChildEmpty)
+                t0 = child_key(mnx.x, mny.x, mnz.x, mxx.x, mxy.x, mxz.x, r, inv, tmin, tmax_entry, closest, prune,
+                               delta);
+            if (c1 != rtdev::kChildEmpty)
+                t1 = child_key(mnx.y, mny.y, mnz.y, mxx.y, mxy.y, mxz.y, r, inv, tmin, tmax_entry, closest, prune,
+                               delta);
+            if (c2 != rtdev::kChildEmpty)
+                t2 = child_key(mnx.z, mny.z, mnz.z, mxx.z, mxy.z, mxz.z, r, inv, tmin, tmax_entry, closest, prune,
+                               delta);
+            if (c3 != rtdev::kChildEmpty)
+                t3 = child_key(mnx.w, mny.w, mnz.w, mxx.w, mxy.w, mxz.w, r, inv, tmin, tmax_entry, closest, prune,
+                               delta);
+        }
         PROF_ADD(kPrBvhTrip, pt);
+        PROF_T0(pp);
         sort2(t0, c0, t1, c1);
         sort2(t2, c2, t3, c3);
         sort2(t0, c0, t2, c2);
@@ -792,8 +821,11 @@ RT_DEV bool bvh_hit(const DevScene& S, float delta, uint32_t root, const Ray& r,
                 sp += 1u;
             }
             cur = c0;
+            PROF_ADD(kPrBvhPush, pp);
             continue;
         }
+        PROF_ADD(kPrBvhPush, pp);
+        PROF_T0(ppop);
         bool found = false;
         while (sp > 0u) {
             sp -= 1u;
@@ -805,8 +837,26 @@ RT_DEV bool bvh_hit(const DevScene& S, float delta, uint32_t root, const Ray& r,
                 break;
             }
         }
+        PROF_ADD(kPrBvhPop, ppop);
         if (!found) break;
     }
+    PROF_ADD(kPrBvhCall, pcall);
+#ifdef RT_PROFILE_REGIONS
+    {
+        const uint32_t b = trips_bin(visits);
+        uint32_t m = visits;
+        for (int off = 32; off > 0; off >>= 1) {
+            uint32_t o = __shfl_xor(m, off);
+            m = o > m ? o : m;
+        }
+        const uint32_t first = (uint32_t)__builtin_ctzll(__ballot(1));
+        for (uint32_t bin = 0; bin < 8u; ++bin) {
+            const uint32_t n = (uint32_t)__popcll(__ballot(b == bin));
+            if (__lane_id() == first && n) prof_lds[3u * kPrCount + bin] += n;
+        }
+        if (__lane_id() == first) prof_lds[3u * kPrCount + 8u + trips_bin(m)] += 1u;
+    }
+#endif
 #ifdef RT_LEAF_AUDIT
     {  // the replay of the reference recursion must agree with the fast traversal
         float c2 = tmax_entry;
@@ -1390,7 +1440,10 @@ RT_DEV bool finish_segment(const DevScene& S, const DevParams& P, const ChunkPar
 // segment count.
 constexpr uint32_t kReplayCap = 1u << 20;
 template <bool kRef>
-__global__ __launch_bounds__(64) void trace_samples(DevScene Sg, DevCamera C, DevParams P, ChunkParams Q,
+#ifndef RT_TRACE_MIN_WAVES
+#define RT_TRACE_MIN_WAVES 1  // waves/SIMD the register allocator must allow (build-time tuning)
+#endif
+__global__ __launch_bounds__(64, RT_TRACE_MIN_WAVES) void trace_samples(DevScene Sg, DevCamera C, DevParams P, ChunkParams Q,
                                                     float* __restrict__ sbuf, TraceCounters* __restrict__ ctr,
                                                     ReplayItem* __restrict__ replay_list, uint32_t fixup,
                                                     unsigned long long* __restrict__ seg_counter) {
@@ -1689,14 +1742,21 @@ int rt_scene_free(rt_scene_handle s) {
     {
         DeviceGuard g(s->device);
 #ifdef RT_PROFILE_REGIONS
-        static unsigned long long hc[kProfCopies * 3 * kPrCount];
-        unsigned long long h[3 * kPrCount] = {};
+        static unsigned long long hc[kProfCopies * kProfWords];
+        unsigned long long h[kProfWords] = {};
         if (hipDeviceSynchronize() == hipSuccess && hipMemcpyFromSymbol(hc, HIP_SYMBOL(g_prof), sizeof hc) == hipSuccess) {
             for (uint32_t c = 0; c < kProfCopies; ++c)
-                for (uint32_t i = 0; i < 3u * kPrCount; ++i) h[i] += hc[c * 3u * kPrCount + i];
+                for (uint32_t i = 0; i < kProfWords; ++i) h[i] += hc[c * kProfWords + i];
             fprintf(stderr, "{\"rt_profile\": [");
             for (uint32_t i = 0; i < 3u * kPrCount; ++i) fprintf(stderr, "%s%llu", i ? "," : "", h[i]);
             fprintf(stderr, "]}\n");
+        }
+        {
+            const unsigned long long* th = h + 3u * kPrCount;
+            fprintf(stderr, "{\"trips_hist\": [%llu,%llu,%llu,%llu,%llu,%llu,%llu,%llu], \"wave_max_hist\": "
+                            "[%llu,%llu,%llu,%llu,%llu,%llu,%llu,%llu]}\n",
+                    th[0], th[1], th[2], th[3], th[4], th[5], th[6], th[7], th[8], th[9], th[10], th[11], th[12],
+                    th[13], th[14], th[15]);
         }
 #endif
 #ifdef RT_LEAF_AUDIT

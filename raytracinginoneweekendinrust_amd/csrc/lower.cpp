@@ -660,8 +660,13 @@ class Lowerer {
         }
         uint32_t base = (uint32_t)(s_->nodes.size() / rtdev::kBvhNodeF4);
         uint32_t total = base + 1 + (uint32_t)wide.size();
-        if (total > rtdev::kMaxIndex) return fail(RT_ERR_UNSUPPORTED, "too many BVH nodes");
+        if (total >= rtdev::kLeafNodeFlag) return fail(RT_ERR_UNSUPPORTED, "too many BVH nodes");
         s_->nodes.resize((size_t)total * rtdev::kBvhNodeF4);
+        auto leaf_node = [&](uint32_t w) {
+            for (const Slot& c : wide[w])
+                if (c.node) return false;
+            return true;
+        };
         auto put = [&](uint32_t o, const std::vector<Slot>& sl, uint32_t flags) {
             float mnx[4], mny[4], mnz[4], mxx[4], mxy[4], mxz[4];
             uint32_t ch[4], rk[4];
@@ -670,7 +675,14 @@ class Lowerer {
                 const Box b = have ? sl[k].box : Box{{0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f}};
                 mnx[k] = b.mn.x; mny[k] = b.mn.y; mnz[k] = b.mn.z;
                 mxx[k] = b.mx.x; mxy[k] = b.mx.y; mxz[k] = b.mx.z;
-                ch[k] = !have ? rtdev::kChildEmpty : sl[k].node ? base + 1 + (sl[k].id & ~0x40000000u) : sl[k].id;
+                if (!have) {
+                    ch[k] = rtdev::kChildEmpty;
+                } else if (sl[k].node) {
+                    const uint32_t w = sl[k].id & ~0x40000000u;
+                    ch[k] = (base + 1 + w) | (leaf_node(w) ? rtdev::kLeafNodeFlag : 0u);
+                } else {
+                    ch[k] = sl[k].id;
+                }
                 rk[k] = have ? sl[k].rank : 0u;
             }
             rk[3] |= flags;

@@ -22,8 +22,9 @@ sys.path.insert(0, ROOT)
 
 NAMES = ["Refill", "Finish segment", "World", "Record", "Emit", "Scatter", "Marble", "Store", "Checker", "Image",
          "UnitSphere", "Dielectric", "Lambert", "Metal", "Isotropic", "MediumLog"]
-COUNT = 48
-EXTRA = {44: "BVH loop trip", 45: "BVH leaf test"}
+COUNT = 52
+EXTRA = {44: "BVH loop trip (child tests)", 45: "BVH leaf test", 46: "BVH call setup", 47: "BVH sort + push",
+         48: "BVH pop loop", 49: "BVH call total"}
 ENTRY0 = 16
 SHOWCASE = ["boxes BVH", "light rect", "moving sphere", "glass sphere", "metal sphere", "medium boundary",
             "blue medium", "fog medium", "earth", "marble", "spheres BVH (RotY+Tr)"]
@@ -61,7 +62,7 @@ def main():
         captured = tf.read().splitlines()
         lines = [ln for ln in captured if ln.startswith('{"rt_profile"')]
         for ln in captured:
-            if ln.startswith(('{"leaf_audit', '{"audit', '{"trav_audit')):
+            if ln.startswith(('{"leaf_audit', '{"audit', '{"trav_audit', '{"trips_hist')):
                 print(ln)
     if not lines:  # an audit build: no region counters
         return
