@@ -166,6 +166,28 @@ int rt_render_launch(rt_scene_handle scene, const rt_camera_desc* camera,
                      const rt_render_params* params, float* d_out,
                      unsigned long long* d_segments, void* stream);
 
+/* One frame over several devices of this process: scenes[i]
+ * (uploaded on its own device; two handles may share a device) renders the 8x8
+ * blocks b with b % n == i, all devices concurrently, and the shards are gathered
+ * into host_out (W*H*3 floats, every pixel written). params->shard_count must be
+ * 0 or 1. stats: segments summed, kernel_ms of the slowest device. The result is
+ * bit-identical to rt_render on one device. */
+int rt_render_multi(rt_scene_handle* scenes, uint32_t n, const rt_camera_desc* camera,
+                    const rt_render_params* params, float* host_out, rt_stats* stats);
+
+/* Output step of Renderer::render (src/renderer.rs:107-127) on the device.
+ * rt_quantize_srgb8: palette 0.6.1 Srgb<f32> -> Srgb<u8> (clamp to [0, 1] with
+ * NaN -> 0, x 255, round half away from zero; no gamma, src/utils.rs:19-23) of a
+ * device image (W*H*3 floats, row 0 = bottom) into d_u8 (W*H*3 bytes, rows top to
+ * bottom, as the PPM writes them); asynchronous on `stream`.
+ * rt_format_ppm: the P3 body the reference prints, "r g b\n" per pixel, rows top
+ * to bottom, into device buffer d_text (capacity >= 12 bytes per pixel); the
+ * "P3\nW H\n255\n" header is not included. Synchronises `stream` and stores the
+ * body length in *text_bytes. */
+int rt_quantize_srgb8(const float* d_rgb, uint8_t* d_u8, uint32_t width, uint32_t height, void* stream);
+int rt_format_ppm(const float* d_rgb, uint32_t width, uint32_t height, char* d_text, uint64_t capacity,
+                  uint64_t* text_bytes, void* stream);
+
 /* Device time of the trace kernel launches issued by rt_render_launch on this
  * scene since the last reset (HIP events recorded on the launch stream around
  * each launch; waits for them). Up to 256 launches are kept between resets. */

@@ -155,3 +155,26 @@ def numeric_eval(op: int, a, b=None) -> np.ndarray:
     lib.oracle_numeric_eval(op, a.ctypes.data_as(C.POINTER(C.c_double)), bp,
                             out.ctypes.data_as(C.POINTER(C.c_double)), a.size)
     return out
+
+
+def srgb8(img: np.ndarray) -> np.ndarray:
+    """palette 0.6.1 `Srgb::<f32>::into_format::<u8>()` per channel, as called by
+    Renderer::write_ppm (src/renderer.rs:116-121; srgb_from_vec3 applies no gamma,
+    src/utils.rs:19-23): scaled = c * 255.0 in f32, f32::round (half away from zero),
+    clamp to [0, 255], `as u8` (NaN -> 0). Rows are returned top to bottom (y = H-1
+    first), the order write_ppm emits them. Restated in the reference's own order
+    (scale, round, clamp), so it also checks the device's clamp-first evaluation."""
+    with np.errstate(over="ignore", invalid="ignore"):   # 3e38 * 255 -> inf, as in f32 on the device
+        s = np.asarray(img, dtype=np.float32)[::-1] * np.float32(255.0)
+    a = np.abs(s).astype(np.float64)          # f32 -> f64 is exact; +0.5 then floor is exact too
+    r = np.copysign(np.floor(a + 0.5), s)
+    r = np.where(r < 0.0, 0.0, np.where(r > 255.0, 255.0, r))
+    return np.nan_to_num(r, nan=0.0).astype(np.uint8)
+
+
+def ppm(img: np.ndarray) -> bytes:
+    """Renderer::write_ppm (src/renderer.rs:107-127): "P3\\nW H\\n255\\n" then "r g b\\n" per pixel."""
+    h, w, _ = img.shape
+    q = srgb8(img).reshape(-1, 3)
+    body = "".join(f"{r} {g} {b}\n" for r, g, b in q.tolist())
+    return f"P3\n{w} {h}\n255\n{body}".encode()

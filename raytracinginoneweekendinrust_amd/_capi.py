@@ -73,6 +73,11 @@ SIGNATURES = [
     ("rt_scene_info", C.c_int, [C.c_void_p, C.POINTER(C.c_uint64)]),
     ("rt_render_launch", C.c_int, [C.c_void_p, C.POINTER(rt_camera_desc), C.POINTER(rt_render_params), C.c_void_p,
                                    C.c_void_p, C.c_void_p]),
+    ("rt_render_multi", C.c_int, [C.POINTER(C.c_void_p), C.c_uint32, C.POINTER(rt_camera_desc),
+                                  C.POINTER(rt_render_params), C.POINTER(C.c_float), C.POINTER(rt_stats)]),
+    ("rt_quantize_srgb8", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p]),
+    ("rt_format_ppm", C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64),
+                                C.c_void_p]),
     ("rt_scene_trace_time", C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_uint64), C.c_int]),
     ("rt_render", C.c_int, [C.c_void_p, C.POINTER(rt_camera_desc), C.POINTER(rt_render_params),
                             C.POINTER(C.c_float), C.POINTER(rt_stats)]),
@@ -89,6 +94,14 @@ def load() -> C.CDLL:
         raise ImportError(
             f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
             "(the MI355X path has no CPU fallback)")
+    # One HIP runtime per process. torch ships its own libamdhip64 (soname libamdhip64.so.7,
+    # file name libamdhip64.so); loading torch first lets librtamd's NEEDED entry bind to that
+    # copy by soname. Loaded the other way round, the process holds two runtimes and whichever
+    # initialises second finds no device.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = C.CDLL(LIB_PATH)
     for name, res, args in SIGNATURES:
         fn = getattr(lib, name)

@@ -1918,6 +1918,7 @@ int rt_render_launch(rt_scene_handle s, const rt_camera_desc* camera, const rt_r
             s->ev_overflow = true;
         }
         if (evp) (void)hipEventRecord(evp[0], st);
+        (void)hipGetLastError();  // hipGetLastError is sticky: drop an unrelated earlier error
         if (exact) {  // every BVH traversed by the literal replay of bvh.rs
             hipLaunchKernelGGL(trace_samples<true>, dim3(grid_ref), dim3(64), lds_ref, st, dev_ref, cam, dp, q,
                                s->sbuf, s->counter, s->replay, 0u, d_segments);
@@ -1992,6 +1993,97 @@ int rt_render(rt_scene_handle s, const rt_camera_desc* camera, const rt_render_p
     return RT_OK;
 }
 
+int rt_render_multi(rt_scene_handle* scenes, uint32_t n, const rt_camera_desc* camera, const rt_render_params* p,
+                    float* host_out, rt_stats* stats) {
+    rthost::clear_error();
+    if (!scenes || n == 0 || !camera || !host_out) return rthost::set_error(RT_ERR_INVALID, "NULL argument or n == 0");
+    int rc = check_params(p);
+    if (rc) return rc;
+    if (p->shard_count > 1) return rthost::set_error(RT_ERR_INVALID, "rt_render_multi shards the frame itself");
+    for (uint32_t i = 0; i < n; ++i)
+        if (!scenes[i]) return rthost::set_error(RT_ERR_INVALID, "NULL scene handle");
+    const size_t floats = (size_t)p->width * p->height * 3u;
+    struct Shard {
+        int device = 0;
+        hipStream_t st = nullptr;
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        float* d_out = nullptr;
+        unsigned long long* d_seg = nullptr;
+        unsigned long long seg = 0;
+        std::vector<float> img;
+    };
+    std::vector<Shard> sh(n);
+    auto cleanup = [&]() {
+        for (Shard& x : sh) {
+            DeviceGuard g(x.device);
+            if (x.st) (void)hipStreamSynchronize(x.st);
+            if (x.e0) (void)hipEventDestroy(x.e0);
+            if (x.e1) (void)hipEventDestroy(x.e1);
+            if (x.st) (void)hipStreamDestroy(x.st);
+            if (x.d_out) (void)hipFree(x.d_out);
+            if (x.d_seg) (void)hipFree(x.d_seg);
+        }
+    };
+    hipError_t e;
+    // launch every shard before waiting for any (devices run concurrently)
+    for (uint32_t i = 0; i < n; ++i) {
+        Shard& x = sh[i];
+        x.device = scenes[i]->device;
+        DeviceGuard g(x.device);
+        if (!g.ok) { cleanup(); return rthost::set_error(RT_ERR_HIP, "hipSetDevice failed"); }
+        if ((e = hipStreamCreateWithFlags(&x.st, hipStreamNonBlocking)) != hipSuccess) { cleanup(); return hip_fail(e, "hipStreamCreate"); }
+        if ((e = hipMalloc(&x.d_out, floats * sizeof(float))) != hipSuccess ||
+            (e = hipMalloc(&x.d_seg, sizeof(unsigned long long))) != hipSuccess) {
+            cleanup();
+            return rthost::set_error(RT_ERR_OOM, "hipMalloc shard image");
+        }
+        if ((e = hipMemsetAsync(x.d_out, 0, floats * sizeof(float), x.st)) != hipSuccess ||
+            (e = hipMemsetAsync(x.d_seg, 0, sizeof(unsigned long long), x.st)) != hipSuccess) {
+            cleanup();
+            return hip_fail(e, "memset");
+        }
+        (void)hipEventCreate(&x.e0);
+        (void)hipEventCreate(&x.e1);
+        (void)hipEventRecord(x.e0, x.st);
+        rt_render_params q = *p;
+        q.shard_index = n > 1 ? i : 0u;
+        q.shard_count = n > 1 ? n : 0u;
+        if ((rc = rt_render_launch(scenes[i], camera, &q, x.d_out, x.d_seg, x.st))) { cleanup(); return rc; }
+        (void)hipEventRecord(x.e1, x.st);
+        x.img.resize(floats);
+        if ((e = hipMemcpyAsync(x.img.data(), x.d_out, floats * sizeof(float), hipMemcpyDeviceToHost, x.st)) != hipSuccess ||
+            (e = hipMemcpyAsync(&x.seg, x.d_seg, sizeof x.seg, hipMemcpyDeviceToHost, x.st)) != hipSuccess) {
+            cleanup();
+            return hip_fail(e, "D2H shard");
+        }
+    }
+    float ms_max = 0.0f;
+    for (Shard& x : sh) {
+        DeviceGuard g(x.device);
+        if ((e = hipStreamSynchronize(x.st)) != hipSuccess) { cleanup(); return hip_fail(e, "render shard"); }
+        float ms = 0.0f;
+        (void)hipEventElapsedTime(&ms, x.e0, x.e1);
+        ms_max = ms > ms_max ? ms : ms_max;
+    }
+    // gather: every 8x8 block comes from the device that rendered it
+    const uint32_t bxn = (p->width + 7u) / 8u;
+    unsigned long long seg = 0;
+    for (uint32_t y = 0; y < p->height; ++y)
+        for (uint32_t x = 0; x < p->width; ++x) {
+            const uint32_t owner = ((y / 8u) * bxn + x / 8u) % n;
+            const size_t o = ((size_t)y * p->width + x) * 3u;
+            memcpy(host_out + o, sh[owner].img.data() + o, 3u * sizeof(float));
+        }
+    for (Shard& x : sh) seg += x.seg;
+    if (stats) {
+        stats->segments = seg;
+        stats->samples = (uint64_t)p->width * p->height * p->samples_per_pixel;
+        stats->kernel_ms = ms_max;
+    }
+    cleanup();
+    return RT_OK;
+}
+
 int rt_scene_trace_time(rt_scene_handle s, double* total_ms, uint64_t* launches, int reset) {
     rthost::clear_error();
     if (!s || !total_ms || !launches) return rthost::set_error(RT_ERR_INVALID, "NULL argument");
@@ -2032,6 +2124,7 @@ int rt_device_numeric_eval(int op, const double* a, const double* b, double* out
     if (e == hipSuccess) e = hipMemcpy(da, a, bytes, hipMemcpyHostToDevice);
     if (e == hipSuccess && b) e = hipMemcpy(db, b, bytes, hipMemcpyHostToDevice);
     if (e == hipSuccess) {
+        (void)hipGetLastError();
         hipLaunchKernelGGL(numeric_eval, dim3((n + 255u) / 256u), dim3(256), 0, nullptr, op, da, db, dout, n);
         e = hipGetLastError();
     }

@@ -4,11 +4,13 @@
 // same background table (:155-164), same image height rule
 // (H = (W as f32 / aspect) as usize, src/renderer.rs:34-39) and the same ASCII
 // P3 PPM on stdout (src/renderer.rs:107-127). The render itself runs on the
-// GPU through the C ABI; there is no CPU fallback.
+// GPU through the C ABI, and so does the output step: the image never leaves
+// the device as floats, rt_format_ppm quantises and formats the P3 body there.
+// There is no CPU fallback.
 //
 // Extra flags (not in the reference): --seed N (the reference's thread_rng is
-// OS-seeded), --assets DIR, --device N, --pfm FILE (linear float dump),
-// --exact-bvh.
+// OS-seeded), --assets DIR, --device N, --devices N (one frame over devices
+// 0..N-1, rt_render_multi), --pfm FILE (linear float dump), --exact-bvh.
 #include <math.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -17,6 +19,8 @@
 #include <chrono>
 #include <string>
 #include <vector>
+
+#include <hip/hip_runtime_api.h>
 
 #include "../../include/rt.h"
 
@@ -41,7 +45,7 @@ void usage() {
             "      --cam-focus-dist <D>         [default: 10]\n"
             "      --cam-start-time <T>         [default: 0]\n"
             "      --cam-end-time <T>           [default: 0]\n"
-            "      --seed <N> --assets <DIR> --device <N> --pfm <FILE> --exact-bvh\n");
+            "      --seed <N> --assets <DIR> --device <N> --devices <N> --pfm <FILE> --exact-bvh\n");
 }
 
 bool parse_f(const char* s, float* out) {
@@ -53,13 +57,6 @@ bool parse_u(const char* s, unsigned long long* out) {
     char* end = nullptr;
     *out = strtoull(s, &end, 10);
     return end && *end == '\0';
-}
-
-// palette 0.6.1 Srgb<f32> -> Srgb<u8> (restated: clamp to [0,1], scale, round).
-unsigned to_u8(float c) {
-    if (!(c > 0.0f)) c = 0.0f;
-    if (c > 1.0f) c = 1.0f;
-    return (unsigned)lroundf(c * 255.0f);
 }
 
 std::string default_assets(const char* argv0) {
@@ -77,7 +74,7 @@ int main(int argc, char** argv) {
         return 2;
     }
     std::string scene;
-    unsigned long long width = 1080, spp = 500, depth = 50, tw = 8, th = 8, seed = 1, device = 0;
+    unsigned long long width = 1080, spp = 500, depth = 50, tw = 8, th = 8, seed = 1, device = 0, devices = 1;
     float aspect[2] = {16.0f, 9.0f};
     float from[3] = {13.0f, 2.0f, 3.0f}, at[3] = {0.0f, 0.0f, 0.0f}, up[3] = {0.0f, 1.0f, 0.0f};
     float vfov = 20.0f, aperture = 0.0f, focus = 10.0f, t0 = 0.0f, t1 = 0.0f;
@@ -123,6 +120,7 @@ int main(int argc, char** argv) {
         else if (a == "--cam-end-time") fl(&t1, 1);
         else if (a == "--seed") ul(&seed);
         else if (a == "--device") ul(&device);
+        else if (a == "--devices") ul(&devices);
         else if (a == "--assets") { need(1); assets = argv[++i]; }
         else if (a == "--pfm") { need(1); pfm = argv[++i]; }
         else if (a == "--exact-bvh") exact = true;
@@ -166,37 +164,63 @@ int main(int argc, char** argv) {
         fprintf(stderr, "error: %s\n", rt_last_error());
         return 1;
     }
-    rt_scene_handle h = nullptr;
-    if (rt_scene_upload(desc, (int)device, &h) != RT_OK) {
-        fprintf(stderr, "error: %s\n", rt_last_error());
+    const unsigned long long ndev = devices < 1 ? 1 : devices;
+    std::vector<rt_scene_handle> handles(ndev, nullptr);
+    auto fail = [&](const char* what) {
+        fprintf(stderr, "error: %s: %s\n", what, rt_last_error());
+        for (rt_scene_handle x : handles)
+            if (x) rt_scene_free(x);
         rt_scene_desc_free(desc);
+        return 1;
+    };
+    for (unsigned long long i = 0; i < ndev; ++i)
+        if (rt_scene_upload(desc, (int)(ndev > 1 ? i : device), &handles[i]) != RT_OK) return fail("rt_scene_upload");
+    const int dev0 = (int)(ndev > 1 ? 0 : device);
+    const size_t npix = (size_t)width * height, fbytes = npix * 3u * sizeof(float);
+    float* d_out = nullptr;
+    char* d_text = nullptr;
+    unsigned long long* d_seg = nullptr;
+    hipStream_t st = nullptr;
+    if (hipSetDevice(dev0) != hipSuccess || hipStreamCreate(&st) != hipSuccess || hipMalloc(&d_out, fbytes) != hipSuccess ||
+        hipMalloc(&d_seg, sizeof *d_seg) != hipSuccess || hipMalloc(&d_text, npix * 12u + 1u) != hipSuccess ||
+        hipMemsetAsync(d_out, 0, fbytes, st) != hipSuccess || hipMemsetAsync(d_seg, 0, sizeof *d_seg, st) != hipSuccess) {
+        fprintf(stderr, "error: device allocation failed\n");
         return 1;
     }
-    std::vector<float> img((size_t)width * height * 3u, 0.0f);
-    rt_stats st;
+    rt_stats st_multi;
+    memset(&st_multi, 0, sizeof st_multi);
+    std::vector<float> img;
     fprintf(stderr, "Rendering tiles...\n");
-    if (rt_render(h, &cam, &p, img.data(), &st) != RT_OK) {
-        fprintf(stderr, "error: %s\n", rt_last_error());
-        rt_scene_free(h);
-        rt_scene_desc_free(desc);
-        return 1;
+    if (ndev > 1) {  // one frame over several devices, gathered on the host, then back to device 0
+        img.assign(npix * 3u, 0.0f);
+        if (rt_render_multi(handles.data(), (uint32_t)ndev, &cam, &p, img.data(), &st_multi) != RT_OK)
+            return fail("rt_render_multi");
+        if (hipMemcpyAsync(d_out, img.data(), fbytes, hipMemcpyHostToDevice, st) != hipSuccess) return fail("H2D");
+    } else if (rt_render_launch(handles[0], &cam, &p, d_out, d_seg, st) != RT_OK) {
+        return fail("rt_render_launch");
     }
     fprintf(stderr, "\nDone tracing.\nWriting to file...\n");
-    std::string outbuf;
-    outbuf.reserve((size_t)width * height * 12u + 32u);
+    uint64_t text_bytes = 0;
+    if (rt_format_ppm(d_out, (uint32_t)width, (uint32_t)height, d_text, npix * 12u + 1u, &text_bytes, st) != RT_OK)
+        return fail("rt_format_ppm");
+    std::string out;
     char line[64];
     snprintf(line, sizeof line, "P3\n%llu %llu\n255\n", width, height);
-    outbuf += line;
-    for (long long y = (long long)height - 1; y >= 0; --y)
-        for (unsigned long long x = 0; x < width; ++x) {
-            const float* c = &img[((size_t)y * width + x) * 3u];
-            snprintf(line, sizeof line, "%u %u %u\n", to_u8(c[0]), to_u8(c[1]), to_u8(c[2]));
-            outbuf += line;
-        }
-    fwrite(outbuf.data(), 1, outbuf.size(), stdout);
+    out = line;
+    const size_t head = out.size();
+    out.resize(head + text_bytes);
+    unsigned long long seg = 0;
+    if (hipMemcpy(&out[head], d_text, text_bytes, hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(&seg, d_seg, sizeof seg, hipMemcpyDeviceToHost) != hipSuccess)
+        return fail("D2H");
+    fwrite(out.data(), 1, out.size(), stdout);
     fflush(stdout);
     fprintf(stderr, "Done writing to file.\n");
     if (!pfm.empty()) {
+        if (img.empty()) {
+            img.resize(npix * 3u);
+            (void)hipMemcpy(img.data(), d_out, fbytes, hipMemcpyDeviceToHost);
+        }
         FILE* f = fopen(pfm.c_str(), "wb");
         if (f) {
             fprintf(f, "PF\n%llu %llu\n-1.0\n", width, height);  // PFM rows are bottom-up, like ours
@@ -204,10 +228,14 @@ int main(int argc, char** argv) {
             fclose(f);
         }
     }
-    rt_scene_free(h);
+    (void)hipFree(d_out);
+    (void)hipFree(d_text);
+    (void)hipFree(d_seg);
+    (void)hipStreamDestroy(st);
+    for (rt_scene_handle x : handles) rt_scene_free(x);
     rt_scene_desc_free(desc);
     double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - start).count();
-    fprintf(stderr, "Render time: %.3fs (kernel %.3f ms, %llu samples, %llu segments)\n", secs, st.kernel_ms,
-            (unsigned long long)st.samples, (unsigned long long)st.segments);
+    fprintf(stderr, "Render time: %.3fs (%llu devices, %llu segments)\n", secs, ndev,
+            ndev > 1 ? (unsigned long long)st_multi.segments : seg);
     return 0;
 }
