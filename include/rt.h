@@ -188,6 +188,16 @@ int rt_quantize_srgb8(const float* d_rgb, uint8_t* d_u8, uint32_t width, uint32_
 int rt_format_ppm(const float* d_rgb, uint32_t width, uint32_t height, char* d_text, uint64_t capacity,
                   uint64_t* text_bytes, void* stream);
 
+/* Bvh::new's leaf order (src/bvh.rs:249-333) built on the device. d_keys holds
+ * n x 3 floats, item i's bounding_box(0, 0).min (the box_compare key, :420-440);
+ * seed is the BVH's split-axis seed (rt_node.seed of its RT_OBJ_BVH node). Writes
+ * to d_order the item indices in the order the reference recursion leaves them
+ * (random axis per node, stable total_cmp sort, split at n / 2, two-item nodes
+ * ordered by one comparison). Synchronises `stream`. rt_scene_upload uses it for
+ * BVHs of >= 16384 items (RT_BVH_BUILD=host|device|auto overrides: "device" builds
+ * every BVH on the device, "host" none); the lowered tree is identical either way. */
+int rt_bvh_build_order(const float* d_keys, uint32_t n, uint64_t seed, uint32_t* d_order, void* stream);
+
 /* Device time of the trace kernel launches issued by rt_render_launch on this
  * scene since the last reset (HIP events recorded on the launch stream around
  * each launch; waits for them). Up to 256 launches are kept between resets. */

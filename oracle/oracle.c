@@ -677,6 +677,40 @@ static int bvh_new_helper(OBvh* b, OSortItem* objs, OSortItem* tmp, int n, float
     return b->n++;
 }
 
+/* The leaf order bvh_new_helper leaves its items in (bvh.rs:249-333), for the
+ * device builder's parity tests: the same axis stream, stable merge sort and
+ * two-item comparison, on items identified by index. */
+static void bvh_order_helper(OSortItem* objs, OSortItem* tmp, int n, OAxisRng* ar) {
+    int axis = axis_draw(ar);
+    if (n == 2) {
+        if (!(total_cmp(objs[0].key[axis], objs[1].key[axis]) < 0)) {
+            OSortItem t = objs[0];
+            objs[0] = objs[1];
+            objs[1] = t;
+        }
+    } else if (n > 2) {
+        merge_sort_axis(objs, tmp, n, axis);
+        int mid = n / 2;
+        bvh_order_helper(objs, tmp, mid, ar);
+        bvh_order_helper(objs + mid, tmp, n - mid, ar);
+    }
+}
+int oracle_bvh_order(const float* keys, uint32_t n, uint64_t seed, uint32_t* order) {
+    if (n == 0) return 0;
+    OSortItem* it = (OSortItem*)malloc(2u * (size_t)n * sizeof(OSortItem));
+    if (!it) return -4;
+    for (uint32_t i = 0; i < n; ++i) {
+        it[i].obj = (const OHit*)(uintptr_t)(i + 1u);
+        for (int k = 0; k < 3; ++k) it[i].key[k] = keys[3u * i + k];
+    }
+    OAxisRng ar;
+    rng_init(&ar.r, seed, 0u, 0u);
+    bvh_order_helper(it, it + n, (int)n, &ar);
+    for (uint32_t i = 0; i < n; ++i) order[i] = (uint32_t)((uintptr_t)it[i].obj - 1u);
+    free(it);
+    return 0;
+}
+
 /* ------------------------------------------------------------------------- */
 /* building the object graph from the IR                                      */
 /* ------------------------------------------------------------------------- */

@@ -87,6 +87,8 @@ void oracle_sphere_uv(const float p[3], float uv[2]);                /* sphere.r
 void oracle_camera_basis(const rt_camera_desc* cam, float out[21]);
 /* Perlin Turbulence value of a Marble seed at p (noise 0.8.2 restatement). */
 double oracle_turbulence(uint32_t seed, const double p[3]);
+/* Leaf order of Bvh::new over n items with box_compare keys keys[3 i + axis] (bvh.rs:249-333). */
+int oracle_bvh_order(const float* keys, uint32_t n, uint64_t seed, uint32_t* order);
 /* Host numeric spec evaluation (ops of rt_device_numeric_eval; 8 = rt_cosf, 9 = rt_tanf). */
 void oracle_numeric_eval(int op, const double* a, const double* b, double* out, uint32_t n);
 

@@ -178,3 +178,15 @@ def ppm(img: np.ndarray) -> bytes:
     q = srgb8(img).reshape(-1, 3)
     body = "".join(f"{r} {g} {b}\n" for r, g, b in q.tolist())
     return f"P3\n{w} {h}\n255\n{body}".encode()
+
+
+lib.oracle_bvh_order.restype = C.c_int
+lib.oracle_bvh_order.argtypes = [C.c_void_p, C.c_uint32, C.c_uint64, C.c_void_p]
+
+
+def bvh_order(keys: np.ndarray, seed: int) -> np.ndarray:
+    """Leaf order of Bvh::new (bvh.rs:249-333) for box_compare keys (n, 3) float32."""
+    keys = np.ascontiguousarray(keys, dtype=np.float32).reshape(-1, 3)
+    out = np.empty(len(keys), dtype=np.uint32)
+    _check(lib.oracle_bvh_order(keys.ctypes.data, len(keys), seed, out.ctypes.data), "oracle_bvh_order")
+    return out

@@ -84,6 +84,7 @@ SIGNATURES = [
     ("rt_scene_generate", C.c_int, [C.c_char_p, C.c_uint64, C.c_char_p, C.POINTER(C.POINTER(rt_scene_desc))]),
     ("rt_scene_desc_free", None, [C.POINTER(rt_scene_desc)]),
     ("rt_scene_background", C.c_int, [C.c_char_p, C.POINTER(C.c_float)]),
+    ("rt_bvh_build_order", C.c_int, [C.c_void_p, C.c_uint32, C.c_uint64, C.c_void_p, C.c_void_p]),
     ("rt_device_numeric_eval", C.c_int, [C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double),
                                          C.POINTER(C.c_double), C.c_uint32]),
 ]

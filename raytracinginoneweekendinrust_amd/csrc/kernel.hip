@@ -1658,7 +1658,13 @@ int rt_scene_upload(const rt_scene_desc* desc, int device, rt_scene_handle* out)
     *out = nullptr;
     rthost::HostScene hs;
     std::string err;
-    int rc = rthost::lower_scene(desc, &hs, &err);  // validate the IR before touching a device
+    // Large BVHs are ordered on the target device (bvh_build.hip); RT_BVH_BUILD=host|device|auto.
+    const char* mode = getenv("RT_BVH_BUILD");
+    int dev = device;
+    rthost::BvhOrderer orderer{16384u, rthost::device_bvh_order, &dev};
+    if (mode && !strcmp(mode, "device")) orderer.min_items = 1u;
+    const bool host_only = mode && !strcmp(mode, "host");
+    int rc = rthost::lower_scene(desc, &hs, &err, host_only ? nullptr : &orderer);
     if (rc) return rthost::set_error(rc, err);
     if (hs.max_stack > 96 || hs.max_stack_ref > 96)
         return rthost::set_error(RT_ERR_UNSUPPORTED, "BVH too deep for the LDS traversal stack");

@@ -208,7 +208,8 @@ struct LeafInfo {
 
 class Lowerer {
    public:
-    Lowerer(const rt_scene_desc* d, HostScene* out, std::string* err) : d_(d), s_(out), err_(err) {}
+    Lowerer(const rt_scene_desc* d, HostScene* out, std::string* err, const BvhOrderer* orderer)
+        : d_(d), s_(out), err_(err), orderer_(orderer) {}
 
     int run() {
         if (!d_ || !d_->nodes || d_->num_nodes == 0) return fail(RT_ERR_INVALID, "empty scene");
@@ -521,6 +522,27 @@ class Lowerer {
             items[i].key[1] = b00.mn.y;
             items[i].key[2] = b00.mn.z;
         }
+        // Large BVHs: the leaf order comes from the device builder; the recursion
+        // below then only shapes the tree (which depends on counts alone) and
+        // draws the same axis stream.
+        bool presorted = false;
+        if (orderer_ && count >= orderer_->min_items) {
+            std::vector<float> keys(3u * (size_t)count);
+            for (uint32_t i = 0; i < count; ++i)
+                for (int k = 0; k < 3; ++k) keys[3u * i + k] = items[i].key[k];
+            std::vector<uint32_t> order(count, UINT32_MAX);
+            std::string e;
+            if ((rc = orderer_->fn(orderer_->ctx, keys.data(), count, n.seed, order.data(), &e))) return fail(rc, e);
+            std::vector<LeafInfo> sorted(count);
+            std::vector<uint8_t> seen(count, 0);
+            for (uint32_t i = 0; i < count; ++i) {
+                if (order[i] >= count || seen[order[i]]) return fail(RT_ERR_HIP, "device BVH order is not a permutation");
+                seen[order[i]] = 1;
+                sorted[i] = items[order[i]];
+            }
+            items.swap(sorted);
+            presorted = true;
+        }
         std::vector<TNode> tn;
         tn.reserve(count * 2 + 1);
         AxisStream ax(n.seed);
@@ -540,7 +562,7 @@ class Lowerer {
                 t.box = box_union(o[0].box01, o[0].box01);
                 t.leaf_box[0] = o[0].box01;
             } else if (cnt == 2) {
-                int a = total_cmp(o[0].key[axis], o[1].key[axis]) < 0 ? 0 : 1;
+                int a = presorted || total_cmp(o[0].key[axis], o[1].key[axis]) < 0 ? 0 : 1;
                 t.child[0] = o[a].code;
                 t.child[1] = o[1 - a].code;
                 t.is_node[0] = t.is_node[1] = false;
@@ -548,9 +570,10 @@ class Lowerer {
                 t.leaf_box[0] = o[a].box01;
                 t.leaf_box[1] = o[1 - a].box01;
             } else {
-                std::stable_sort(o, o + cnt, [axis](const LeafInfo& p, const LeafInfo& q) {
-                    return total_cmp(p.key[axis], q.key[axis]) < 0;
-                });
+                if (!presorted)
+                    std::stable_sort(o, o + cnt, [axis](const LeafInfo& p, const LeafInfo& q) {
+                        return total_cmp(p.key[axis], q.key[axis]) < 0;
+                    });
                 uint32_t mid = cnt / 2;
                 uint32_t l = helper(o, mid, depth + 1);
                 uint32_t r = helper(o + mid, cnt - mid, depth + 1);
@@ -780,6 +803,7 @@ class Lowerer {
     const rt_scene_desc* d_;
     HostScene* s_;
     std::string* err_;
+    const BvhOrderer* orderer_ = nullptr;
     std::vector<rtdev::DevEntry> aux_;
     std::unordered_map<int, uint32_t> tex_memo_, mat_memo_, prim_memo_, phase_memo_;
     uint32_t max_depth_ = 0;
@@ -791,9 +815,43 @@ class Lowerer {
 
 }  // namespace
 
-int lower_scene(const rt_scene_desc* desc, HostScene* out, std::string* err) {
+void bvh_split_schedule(uint32_t n, uint64_t seed, BvhSchedule* out) {
+    // The recursion of BvhNode::new_helper (bvh.rs:249-333) without the sorting:
+    // one axis draw per node in preorder; nodes of > 2 items split at n / 2.
+    std::vector<std::vector<uint32_t>> lv;  // per depth: start, count, axis triples
+    AxisStream ax(seed);
+    struct Frame {
+        uint32_t start, count, depth;
+    };
+    std::vector<Frame> st;
+    if (n) st.push_back({0u, n, 0u});
+    while (!st.empty()) {
+        Frame f = st.back();
+        st.pop_back();
+        const uint32_t axis = (uint32_t)ax.axis();
+        if (lv.size() <= f.depth) lv.resize(f.depth + 1);
+        lv[f.depth].insert(lv[f.depth].end(), {f.start, f.count, axis});
+        if (f.count > 2) {
+            const uint32_t mid = f.count / 2;
+            st.push_back({f.start + mid, f.count - mid, f.depth + 1});  // right after the left subtree
+            st.push_back({f.start, mid, f.depth + 1});
+        }
+    }
+    *out = BvhSchedule();
+    out->level_off.push_back(0);
+    for (const auto& v : lv) {
+        for (size_t i = 0; i < v.size(); i += 3) {
+            out->start.push_back(v[i]);
+            out->count.push_back(v[i + 1]);
+            out->axis.push_back(v[i + 2]);
+        }
+        out->level_off.push_back((uint32_t)out->start.size());
+    }
+}
+
+int lower_scene(const rt_scene_desc* desc, HostScene* out, std::string* err, const BvhOrderer* orderer) {
     *out = HostScene();
-    Lowerer l(desc, out, err);
+    Lowerer l(desc, out, err, orderer);
     int rc = l.run();
     out->coord_bound += l.translate_sum();
     return rc;

@@ -108,3 +108,48 @@ def test_invalid_camera_time_range(rt, orc):
     cam = rt.Camera.new((13, 2, 3), (0, 0, 0), (0, 1, 0), 20, 1.7, 0, 10, 1.0, 0.0)
     with pytest.raises(RuntimeError):
         orc.render(scene, cam, params)
+
+
+def _py_bvh_order(keys, seed):
+    """BvhNode::new_helper's leaf order (src/bvh.rs:249-333) in plain Python: axis per node
+    in preorder from the Philox stream (rand 0.8.5 sample_single_inclusive(0, 2)),
+    stable sort by f32 total_cmp (Python's sort is stable), two-item nodes by one compare."""
+    import struct
+    from oracle_ffi import philox
+
+    def tkey(f):
+        u = struct.unpack("<I", struct.pack("<f", f))[0]
+        return u ^ (0xFFFFFFFF if u >> 31 else 0x80000000)
+
+    words, block = [], [0]
+
+    def axis():
+        while True:
+            if not words:
+                words.extend(philox([block[0], 0, 0, 0], [seed & 0xFFFFFFFF, seed >> 32]))
+                block[0] += 1
+            m = words.pop(0) * 3
+            if (m & 0xFFFFFFFF) <= (3 << 30) - 1:
+                return m >> 32
+
+    def helper(items):
+        a = axis()
+        if len(items) == 2:
+            return items if tkey(keys[items[0]][a]) < tkey(keys[items[1]][a]) else items[::-1]
+        if len(items) == 1:
+            return items
+        items = sorted(items, key=lambda i: tkey(keys[i][a]))
+        mid = len(items) // 2
+        return helper(items[:mid]) + helper(items[mid:])
+
+    return helper(list(range(len(keys))))
+
+
+@pytest.mark.parametrize("n,seed", [(1, 3), (2, 3), (3, 1), (9, 20231), (40, 7), (300, 2**33 + 5)])
+def test_oracle_bvh_order_matches_python_restatement(n, seed, orc):
+    rng = np.random.default_rng(n)
+    keys = rng.integers(-2, 3, size=(n, 3)).astype(np.float32)  # many ties
+    keys[::5, 0] = -0.0
+    got = orc.bvh_order(keys, seed)
+    want = _py_bvh_order([tuple(float(x) for x in r) for r in keys], seed)
+    assert list(got) == want
