@@ -72,7 +72,9 @@ typedef enum rt_node_kind {
     RT_OBJ_LIST = 39,         /* ref[0] first index into list_items, ref[1] count
                                                                      hittable.rs:84-98   */
     RT_OBJ_BVH = 40,          /* ref[0] LIST node, f[0] time0, f[1] time1,
-                                 seed = split-axis stream seed        bvh.rs:46-62        */
+                                 seed = split-axis stream seed        bvh.rs:46-62
+                                 ref[1] = 1: Bvh::with_predictor (an HRPP table,
+                                 used only under RT_FLAG_HRPP)        bvh.rs:69-80        */
     RT_OBJ_TRANSLATE = 41,    /* ref[0] child, f[0..3] displacement  instance.rs:23      */
     RT_OBJ_ROTATE_Y = 42,     /* ref[0] child, f[0] degrees          instance.rs:63      */
     RT_OBJ_CONSTANT_MEDIUM = 43 /* ref[0] boundary, ref[1] phase albedo texture,
@@ -114,6 +116,13 @@ typedef struct rt_camera_desc {
 #define RT_FLAG_EXACT_BVH 1u  /* box tests use the BVH entry t_max like bvh.rs:363-417
                                  (no closest-hit pruning); results are identical
                                  except for measure-zero ties, it is slower      */
+#define RT_FLAG_HRPP 2u       /* EXPERIMENT, approximate: hash-based ray path
+                                 prediction on every Bvh::with_predictor BVH
+                                 (src/hrpp.rs, src/bvh.rs:114-211), traversal
+                                 otherwise as RT_FLAG_EXACT_BVH. Tables start
+                                 empty at each launch and are filled concurrently,
+                                 so results are NOT deterministic (neither are
+                                 the reference's, bvh.rs:146-149)             */
 
 typedef struct rt_render_params {
     uint32_t width, height;      /* image size (Renderer::from_aspect_ratio)        */
@@ -198,6 +207,12 @@ int rt_format_ppm(const float* d_rgb, uint32_t width, uint32_t height, char* d_t
  * every BVH on the device, "host" none); the lowered tree is identical either way. */
 int rt_bvh_build_order(const float* d_keys, uint32_t n, uint64_t seed, uint32_t* d_order, void* stream);
 
+/* HRPP statistics of the last RT_FLAG_HRPP render (src/hrpp.rs:91-127): for
+ * predictor p (in lowering order) out[6 p + 0..5] = true-positive, false-positive
+ * and no-prediction BVH calls, table entries (distinct ray hashes), predicted nodes
+ * stored, insertions dropped (table or node set full). *count = predictors. */
+int rt_scene_hrpp_stats(rt_scene_handle scene, uint64_t* out, uint32_t capacity, uint32_t* count);
+
 /* Device time of the trace kernel launches issued by rt_render_launch on this
  * scene since the last reset (HIP events recorded on the launch stream around
  * each launch; waits for them). Up to 256 launches are kept between resets. */
@@ -221,7 +236,8 @@ int rt_scene_background(const char* name, float rgb[3]);
 
 /* Device numeric self-check (diagnostic): evaluates op on `n` inputs on the GPU.
  * op: 0 sqrt f64, 1 sqrt f32, 2 div f32, 3 rt_sinf, 4 rt_acosf, 5 rt_atan2f,
- *     6 rt_logf, 7 div f64. Results are returned as doubles. */
+ *     6 rt_logf, 7 div f64, 8 HRPP map_float_to_hash (hrpp.rs:136-170, six bits).
+ * Results are returned as doubles. */
 int rt_device_numeric_eval(int op, const double* a, const double* b, double* out,
                            uint32_t n);
 

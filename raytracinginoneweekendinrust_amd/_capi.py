@@ -21,6 +21,7 @@ RT_MAT_LAMBERTIAN, RT_MAT_METAL, RT_MAT_DIELECTRIC, RT_MAT_DIFFUSE_LIGHT, RT_MAT
  RT_OBJ_LIST, RT_OBJ_BVH, RT_OBJ_TRANSLATE, RT_OBJ_ROTATE_Y, RT_OBJ_CONSTANT_MEDIUM) = range(32, 44)
 
 RT_FLAG_EXACT_BVH = 1
+RT_FLAG_HRPP = 2
 
 STATUS = {0: "RT_OK", -1: "RT_ERR_INVALID", -2: "RT_ERR_UNSUPPORTED", -3: "RT_ERR_HIP", -4: "RT_ERR_OOM",
           -5: "RT_ERR_NO_DEVICE", -6: "RT_ERR_IO"}
@@ -84,6 +85,7 @@ SIGNATURES = [
     ("rt_scene_generate", C.c_int, [C.c_char_p, C.c_uint64, C.c_char_p, C.POINTER(C.POINTER(rt_scene_desc))]),
     ("rt_scene_desc_free", None, [C.POINTER(rt_scene_desc)]),
     ("rt_scene_background", C.c_int, [C.c_char_p, C.POINTER(C.c_float)]),
+    ("rt_scene_hrpp_stats", C.c_int, [C.c_void_p, C.POINTER(C.c_uint64), C.c_uint32, C.POINTER(C.c_uint32)]),
     ("rt_bvh_build_order", C.c_int, [C.c_void_p, C.c_uint32, C.c_uint64, C.c_void_p, C.c_void_p]),
     ("rt_device_numeric_eval", C.c_int, [C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double),
                                          C.POINTER(C.c_double), C.c_uint32]),

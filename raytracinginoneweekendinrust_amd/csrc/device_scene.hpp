@@ -110,6 +110,16 @@ static_assert(sizeof(DevTexture) == 32, "DevTexture layout");
 //          when every leaf is a Sphere/Rect/Cube, its rank[2] the BVH2 wrapper.
 //   node2: 64 B reference BVH2 node: (Lmin, Lmax.x) (Lmax.yz, Rmin.xy) (Rmin.z,
 //          Rmax) (left, right, 0, 0), DFS preorder behind a wrapper (child 0 = root).
+// One HRPP table slot (32 B): a 48-bit ray hash (hrpp.rs:172-193; ~0 = empty) and
+// up to kHrppIds predicted leaf nodes (the reference keeps an unbounded set; the
+// paper's implementation, which hrpp.rs:62 cites, keeps 5).
+constexpr uint32_t kHrppIds = 6;
+constexpr uint32_t kHrppMaxPredictors = 8;
+struct HrppSlot {
+    unsigned long long key;
+    uint32_t ids[kHrppIds];
+};
+
 struct DevScene {
     const DevEntry* entries;
     const f4* sph;
@@ -127,6 +137,14 @@ struct DevScene {
     uint32_t num_entries;
     uint32_t stack_depth;  // LDS traversal stack entries per lane
     uint32_t perm_bytes;   // size of perm[] (staged in LDS when it fits)
+    // HRPP experiment (RT_FLAG_HRPP; null otherwise). Predictor p (1-based, in the
+    // BVH2 wrapper's row 3 .z) owns table slots [(p - 1) << hrpp_bits, p << hrpp_bits).
+    HrppSlot* hrpp_tab;
+    const unsigned long long* hrpp_keys;  // sorted (wrapper2 << 32 | leaf code)
+    const uint32_t* hrpp_vals;            // -> wrapper-format record of the leaf node
+    unsigned long long* hrpp_stats;       // per predictor: tp, fp, np, dropped
+    uint32_t* hrpp_cnt;                   // per-wave LDS counters (set in the kernel)
+    uint32_t hrpp_bits, hrpp_nkeys, hrpp_npred, pad0;
 };
 
 // Camera::new (camera.rs:44-81) evaluated on the host.

@@ -550,7 +550,7 @@ RT_DEV bool leaf_box_may_hit(float x0, float y0, float z0, float x1, float y1, f
 // node's box with the BVH's entry t_max, the left child (an Index child with
 // t_max, a Hittable with t_max), then the right child (an Index child with
 // t_max, a Hittable with the left hit's t), and `if left.t < right.t {left}
-// else {right}`. The reference kernel (trace_samples<true>) traverses every BVH
+// else {right}`. The reference kernel (trace_samples<1>) traverses every BVH
 // this way: RT_FLAG_EXACT_BVH renders, and the samples the fast kernel hands
 // over because one of their rays could take a NaN hit (with a NaN t in play the
 // tree-min is neither associative nor order-independent, so only the
@@ -661,6 +661,91 @@ RT_DEV bool bvh_hit_reference(const DevScene& S, uint32_t wrapper2, const Ray& r
     return rh;
 }
 
+// ---------------------------------------------------------------------------
+// HRPP experiment (RT_FLAG_HRPP): hash-based ray path prediction, src/hrpp.rs +
+// src/bvh.rs:114-211. Approximate by design; never on the parity path.
+// ---------------------------------------------------------------------------
+// hrpp.rs:136-170, BitPrecision::Six: sign | top 6 exponent bits | top 6 mantissa bits.
+RT_DEV uint32_t hrpp_map_float(float v) {
+    const uint32_t b = __float_as_uint(v);
+    return ((b >> 31) << 15) | (((b >> 25) & 0x3fu) << 7) | ((b >> 17) & 0x3fu);
+}
+// hrpp.rs:172-193: the ray passed to Bvh::hit (its frame, unnormalised direction).
+RT_DEV unsigned long long hrpp_hash(const Ray& r) {
+    const unsigned long long h0 = hrpp_map_float(r.o.x) ^ hrpp_map_float(r.d.z);
+    const unsigned long long h1 = hrpp_map_float(r.o.y) ^ hrpp_map_float(r.d.y);
+    const unsigned long long h2 = hrpp_map_float(r.o.z) ^ hrpp_map_float(r.d.x);
+    return h0 | (h1 << 16) | (h2 << 32);
+}
+// Open addressing, linear probing (32 probes); the slot's key is claimed by CAS.
+RT_DEV rtdev::HrppSlot* hrpp_find(rtdev::HrppSlot* tab, uint32_t bits, unsigned long long key, bool insert) {
+    const uint32_t mask = (1u << bits) - 1u;
+    unsigned long long m = key * 0x9E3779B97F4A7C15ull;
+    const uint32_t h = (uint32_t)(m >> 32) ^ (uint32_t)m;
+    for (uint32_t i = 0; i < 32u; ++i) {
+        rtdev::HrppSlot* sl = tab + ((h + i) & mask);
+        unsigned long long k = __hip_atomic_load(&sl->key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (k == key) return sl;
+        if (k == ~0ull) {
+            if (!insert) return nullptr;
+            k = atomicCAS(&sl->key, ~0ull, key);
+            if (k == ~0ull || k == key) return sl;
+        }
+    }
+    return nullptr;
+}
+RT_DEV uint32_t hrpp_leaf_node(const DevScene& S, unsigned long long k) {  // sorted-map lookup
+    uint32_t lo = 0, hi = S.hrpp_nkeys;
+    while (lo < hi) {
+        const uint32_t m = (lo + hi) >> 1;
+        if (S.hrpp_keys[m] < k) lo = m + 1;
+        else hi = m;
+    }
+    return lo < S.hrpp_nkeys && S.hrpp_keys[lo] == k ? S.hrpp_vals[lo] : 0xffffffffu;
+}
+// Bvh::hit with a predictor (bvh.rs:120-211, GO_UP_LEVEL = 0). Counters per wave
+// in LDS: true positive, false positive, no prediction, dropped insertions.
+RT_DEV bool bvh_hit_hrpp(const DevScene& S, uint32_t wrapper2, uint32_t pid, const Ray& r,
+                                          const RayD& q, V inv, float tmin, float& closest, uint32_t& hit_code,
+                                          uint32_t* stk) {
+    rtdev::HrppSlot* tab = S.hrpp_tab + ((size_t)(pid - 1u) << S.hrpp_bits);
+    uint32_t* cnt = S.hrpp_cnt + 4u * (pid - 1u);
+    const unsigned long long key = hrpp_hash(r);
+    const rtdev::HrppSlot* sl = S.hrpp_bits ? hrpp_find(tab, S.hrpp_bits, key, false) : nullptr;
+    bool predicted = false;
+    if (sl) {  // bvh.rs:141-173: the closest hit among the predicted nodes
+        float c = closest;
+        uint32_t code = 0u;
+        bool any = false;
+        for (uint32_t j = 0; j < rtdev::kHrppIds; ++j) {
+            const uint32_t w = __hip_atomic_load(&sl->ids[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (w == 0xffffffffu) break;
+            predicted = true;
+            if (bvh_hit_reference(S, w, r, q, inv, tmin, c, code, stk)) any = true;
+        }
+        if (any) {  // true positive: traversal skipped (possibly not the closest hit)
+            atomicAdd(&cnt[0], 1u);
+            closest = c;
+            hit_code = code;
+            return true;
+        }
+    }
+    atomicAdd(&cnt[predicted ? 1u : 2u], 1u);  // false positive / no prediction: full traversal
+    const bool h = bvh_hit_reference(S, wrapper2, r, q, inv, tmin, closest, hit_code, stk);
+    if (h && S.hrpp_bits) {  // predictor.insert(ray, leaf node), bvh.rs:188-205
+        const uint32_t leaf = hrpp_leaf_node(S, (unsigned long long)wrapper2 << 32 | hit_code);
+        rtdev::HrppSlot* ins = leaf != 0xffffffffu ? hrpp_find(tab, S.hrpp_bits, key, true) : nullptr;
+        bool ok = false;
+        if (ins)
+            for (uint32_t j = 0; j < rtdev::kHrppIds && !ok; ++j) {
+                const uint32_t old = atomicCAS(&ins->ids[j], 0xffffffffu, leaf);
+                ok = old == 0xffffffffu || old == leaf;
+            }
+        if (!ok) atomicAdd(&cnt[3], 1u);
+    }
+    return h;
+}
+
 // One interior child of a BVH4 node: the reference's box test (stored box, the
 // t_max the BVH was entered with) and, when pruning, the inflated-entry bound.
 // Returns the sort key: the entry distance, +inf when the child is not visited.
@@ -680,12 +765,13 @@ RT_DEV void sort2(float& ta, uint32_t& ca, float& tb, uint32_t& cb) {
         uint32_t c = ca; ca = cb; cb = c;
     }
 }
-// kRef: the reference kernel replays bvh.rs literally. The fast kernel
+// kKind 0: the fast BVH4 kernel; 1: the reference kernel replays bvh.rs literally;
+// 2: the reference kernel with HRPP predictors (RT_FLAG_HRPP experiment). The fast kernel
 // returns with `replay` set for a ray that could take a NaN hit: a ray parallel
 // to an axis plane (a zero direction component) gets t = (k - o) / d = 0 / 0 from
 // a rect whose plane holds its origin, and every comparison against NaN passes
 // (rectangle.rs:36-65); its sample is re-traced by the reference kernel.
-template <bool kRef>
+template <int kKind>
 RT_DEV bool bvh_hit(const DevScene& S, float delta, uint32_t root, const Ray& r, float tmin, float& closest,
                     uint32_t& hit_code, uint32_t* stk, uint32_t mode, bool& replay) {
     PROF_T0(pcall);
@@ -694,8 +780,13 @@ RT_DEV bool bvh_hit(const DevScene& S, float delta, uint32_t root, const Ray& r,
     const f4* wrapper = S.nodes + (size_t)root * rtdev::kBvhNodeF4;
     const V inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
     const RayD q = to_d(r);
-    if constexpr (kRef) {
-        return bvh_hit_reference(S, __float_as_uint(wrapper[7].z), r, q, inv, tmin, closest, hit_code, stk);
+    if constexpr (kKind != 0) {
+        const uint32_t w2 = __float_as_uint(wrapper[7].z);
+        if constexpr (kKind == 2) {
+            const uint32_t pid = __float_as_uint(S.nodes2[4 * (size_t)w2 + 3].z);
+            if (pid) return bvh_hit_hrpp(S, w2, pid, r, q, inv, tmin, closest, hit_code, stk);
+        }
+        return bvh_hit_reference(S, w2, r, q, inv, tmin, closest, hit_code, stk);
     }
     if (r.d.x == 0.0f || r.d.y == 0.0f || r.d.z == 0.0f) {
         replay = true;
@@ -893,20 +984,20 @@ RT_DEV Ray apply_op(f4 op, Ray r) {
 }
 
 // A GEOM or BVH entry (the caller guarantees E is wave-uniform).
-template <bool kRef>
+template <int kKind>
 RT_DEV bool entry_geom_hit(const DevScene& S, float delta, const DevEntry* E, Ray r, float tmin, float& closest,
                            uint32_t& hit_code, uint32_t* stk, uint32_t mode, bool& replay) {
     uint32_t ntf = E->ntf;
     for (uint32_t i = 0; i < ntf; ++i) r = apply_op(E->tf[i], r);
     if (E->kind == rtdev::kEntBvh)
-        return bvh_hit<kRef>(S, delta, E->payload, r, tmin, closest, hit_code, stk, mode, replay);
+        return bvh_hit<kKind>(S, delta, E->payload, r, tmin, closest, hit_code, stk, mode, replay);
     RayD q = to_d(r);
     return leaf_hit(S, E->payload, r, q, tmin, closest, hit_code);
 }
 
 // ConstantMedium::hit (hittable.rs:176-233); draws one U(0,1) once the clamped
 // interval is non-empty, exactly where the reference does.
-template <bool kRef>
+template <int kKind>
 RT_DEV bool medium_hit(const DevScene& S, float delta, const DevEntry* E, Ray r, float tmin, float tmax, Rng& g,
                        const Key& k, float& t_out, uint32_t* stk, uint32_t mode, bool& replay) {
     uint32_t ntf = E->ntf;
@@ -924,8 +1015,8 @@ RT_DEV bool medium_hit(const DevScene& S, float delta, const DevEntry* E, Ray r,
         if (!sphere_select(R, t1 + 0.0001f, kInf, t2)) return false;
     } else {
         uint32_t dummy;
-        if (!entry_geom_hit<kRef>(S, delta, B, r, -kInf, t1, dummy, stk, mode, replay)) return false;
-        if (!entry_geom_hit<kRef>(S, delta, B, r, t1 + 0.0001f, t2, dummy, stk, mode, replay)) return false;
+        if (!entry_geom_hit<kKind>(S, delta, B, r, -kInf, t1, dummy, stk, mode, replay)) return false;
+        if (!entry_geom_hit<kKind>(S, delta, B, r, t1 + 0.0001f, t2, dummy, stk, mode, replay)) return false;
     }
     if (t1 < tmin) t1 = tmin;
     if (t2 > tmax) t2 = tmax;
@@ -1260,7 +1351,7 @@ struct ChunkParams {
 };
 
 // HittableList::hit over the world (hittable.rs:100-118), t in [0.001, inf).
-template <bool kRef>
+template <int kKind>
 RT_DEV bool world_hit(const DevScene& S, float delta, const Ray& r, Rng& g, const Key& k, float& t_hit,
                       uint32_t& hit_entry, uint32_t& hit_code, uint32_t* stk, uint32_t mode, bool& replay) {
     float closest = kInf;
@@ -1270,7 +1361,7 @@ RT_DEV bool world_hit(const DevScene& S, float delta, const Ray& r, Rng& g, cons
         PROF_T0(pe);
         if (E->kind == rtdev::kEntMedium) {
             float t;
-            if (medium_hit<kRef>(S, delta, E, r, 0.001f, closest, g, k, t, stk, mode, replay)) {
+            if (medium_hit<kKind>(S, delta, E, r, 0.001f, closest, g, k, t, stk, mode, replay)) {
                 closest = t;
                 hit_entry = e;
                 hit_code = rtdev::leaf_code(rtdev::kLeafMedium, 0);
@@ -1278,7 +1369,7 @@ RT_DEV bool world_hit(const DevScene& S, float delta, const Ray& r, Rng& g, cons
             }
         } else {
             uint32_t code;
-            if (entry_geom_hit<kRef>(S, delta, E, r, 0.001f, closest, code, stk, mode, replay)) {
+            if (entry_geom_hit<kKind>(S, delta, E, r, 0.001f, closest, code, stk, mode, replay)) {
                 hit_entry = e;
                 hit_code = code;
                 any = true;
@@ -1428,10 +1519,10 @@ RT_DEV bool finish_segment(const DevScene& S, const DevParams& P, const ChunkPar
 // Every live lane traces one whole segment per loop trip: the list walk with its
 // BVH traversals inline, then finish_segment.
 //
-// trace_samples<false> is the fast kernel (BVH4, nearest-first, exact pruning).
+// trace_samples<0> is the fast kernel (BVH4, nearest-first, exact pruning).
 // A sample whose ray could take a NaN hit in a BVH is handed to the reference
 // kernel instead: it is dropped here (its partial segments uncounted) and listed
-// in `replay`. trace_samples<true> traverses every BVH with the literal replay
+// in `replay`. trace_samples<1> traverses every BVH with the literal replay
 // of bvh.rs; it renders whole chunks under RT_FLAG_EXACT_BVH (fixup == 0) and
 // otherwise re-traces the listed samples from their camera ray (fixup == 1).
 // Samples are independent and keyed by (pixel, global sample index), so the
@@ -1439,7 +1530,7 @@ RT_DEV bool finish_segment(const DevScene& S, const DevParams& P, const ChunkPar
 // fixup kernel re-renders the whole chunk and takes back the fast kernel's
 // segment count.
 constexpr uint32_t kReplayCap = 1u << 20;
-template <bool kRef>
+template <int kKind>
 #ifndef RT_TRACE_MIN_WAVES
 #define RT_TRACE_MIN_WAVES 1  // waves/SIMD the register allocator must allow (build-time tuning)
 #endif
@@ -1460,13 +1551,19 @@ __global__ __launch_bounds__(64, RT_TRACE_MIN_WAVES) void trace_samples(DevScene
         __syncthreads();
         S.perm = reinterpret_cast<const uint8_t*>(tab);
     }
+    if (kKind == 2) {  // HRPP counters behind the stack and the Perlin tables
+        const uint32_t perm_words = S.perm_bytes != 0u && S.perm_bytes <= kPermLdsMax ? S.perm_bytes / 4u : 0u;
+        S.hrpp_cnt = lds_stack + S.stack_depth * 128u + perm_words;
+        if (lane < 4u * S.hrpp_npred) S.hrpp_cnt[lane] = 0u;
+        __syncthreads();
+    }
     const Key k{P.seed_lo, P.seed_hi};
     const uint32_t mode = P.tune;
     // item source: the chunk's block batches, or (fixup) the replay list
     unsigned* counter = &ctr->batch;
     const ReplayItem* list = nullptr;
     uint32_t list_n = 0u;
-    if (kRef && fixup) {
+    if (kKind == 1 && fixup) {
         const uint32_t n = __hip_atomic_load(&ctr->replay_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (n <= kReplayCap) {
             if (n == 0u) return;
@@ -1503,9 +1600,9 @@ __global__ __launch_bounds__(64, RT_TRACE_MIN_WAVES) void trace_samples(DevScene
             uint32_t he = 0, hc = 0;
             bool replay = false;
             PROF_T0(pw);
-            bool any = world_hit<kRef>(S, P.prune_delta, ray, g, k, t, he, hc, stk, mode, replay);
+            bool any = world_hit<kKind>(S, P.prune_delta, ray, g, k, t, he, hc, stk, mode, replay);
             PROF_ADD(kPrWorld, pw);
-            if (!kRef && replay) {  // hand the sample to the reference kernel
+            if (kKind == 0 && replay) {  // hand the sample to the reference kernel
                 unsigned idx = atomicAdd(&ctr->replay_count, 1u);
                 if (idx < kReplayCap) replay_list[idx] = ReplayItem{pixel, s_local};
                 has = false;
@@ -1515,12 +1612,16 @@ __global__ __launch_bounds__(64, RT_TRACE_MIN_WAVES) void trace_samples(DevScene
             }
         }
     }
+    if (kKind == 2) {
+        __syncthreads();
+        if (lane < 4u * S.hrpp_npred) atomicAdd(&S.hrpp_stats[lane], (unsigned long long)S.hrpp_cnt[lane]);
+    }
     if (seg_counter) {
         unsigned long long v = nseg;
         for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
         if (lane == 0u) {
             atomicAdd(seg_counter, v);
-            if (!kRef) atomicAdd(&ctr->fast_segments, v);
+            if (kKind == 0) atomicAdd(&ctr->fast_segments, v);
         }
     }
     PROF_FLUSH();
@@ -1564,6 +1665,7 @@ __global__ void numeric_eval(int op, const double* a, const double* b, double* o
         case 5: r = (double)rt_atan2f((float)x, (float)y); break;
         case 6: r = (double)rt_logf((float)x); break;
         case 7: r = x / y; break;
+        case 8: r = (double)hrpp_map_float((float)x); break;
         default: r = 0.0; break;
     }
     out[i] = r;
@@ -1574,6 +1676,31 @@ __global__ void numeric_eval(int op, const double* a, const double* b, double* o
 // ===========================================================================
 // C ABI (device half)
 // ===========================================================================
+namespace {
+// Table occupancy per predictor: out[2 p] = keys, out[2 p + 1] = stored leaf nodes.
+__global__ __launch_bounds__(256) void hrpp_count(const rtdev::HrppSlot* __restrict__ tab, uint32_t bits, uint32_t np,
+                                                  unsigned long long* __restrict__ out) {
+    const uint64_t per = 1ull << bits;
+    for (uint32_t p = 0; p < np; ++p) {
+        unsigned long long keys = 0, ids = 0;
+        for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < per; i += (uint64_t)gridDim.x * 256u) {
+            const rtdev::HrppSlot& sl = tab[(uint64_t)p * per + i];
+            if (sl.key == ~0ull) continue;
+            keys += 1;
+            for (uint32_t j = 0; j < rtdev::kHrppIds; ++j) ids += sl.ids[j] != 0xffffffffu ? 1u : 0u;
+        }
+        for (int off = 32; off > 0; off >>= 1) {
+            keys += __shfl_xor(keys, off);
+            ids += __shfl_xor(ids, off);
+        }
+        if ((threadIdx.x & 63u) == 0u) {
+            atomicAdd(&out[2 * p], keys);
+            atomicAdd(&out[2 * p + 1], ids);
+        }
+    }
+}
+}  // namespace
+
 struct rt_scene {
     int device = 0;
     void* pool = nullptr;
@@ -1585,10 +1712,15 @@ struct rt_scene {
     float* sbuf = nullptr;
     uint64_t sbuf_bytes = 0;
     TraceCounters* counter = nullptr;
-    uint32_t stack_ref = 1;  // LDS stack entries per lane of trace_samples<true> (dev.stack_depth: <false>)
-    int grid = 0, grid_ref = 0;  // resident waves of trace_samples<false> / <true>
+    uint32_t stack_ref = 1;  // LDS stack entries per lane of trace_samples<1, 2> (dev.stack_depth: <0>)
+    int grid = 0, grid_ref = 0;  // resident waves of trace_samples<0> / <1>
     ReplayItem* replay = nullptr;  // kReplayCap entries
     float coord_bound = 0.0f;
+    // HRPP experiment: tables (allocated at the first RT_FLAG_HRPP render) and counters
+    rtdev::HrppSlot* hrpp_tab = nullptr;
+    uint64_t hrpp_tab_bytes = 0;
+    uint32_t hrpp_bits = 0;
+    unsigned long long* hrpp_stats = nullptr;  // kHrppMaxPredictors x 4
     // HIP events bracketing every trace launch (rt_scene_trace_time)
     static constexpr int kEvents = 256;
     hipEvent_t ev[kEvents][2] = {};
@@ -1669,6 +1801,8 @@ int rt_scene_upload(const rt_scene_desc* desc, int device, rt_scene_handle* out)
     if (hs.max_stack > 96 || hs.max_stack_ref > 96)
         return rthost::set_error(RT_ERR_UNSUPPORTED, "BVH too deep for the LDS traversal stack");
     if ((rc = check_device(device))) return rc;
+    if (hs.num_predictors > rtdev::kHrppMaxPredictors)
+        return rthost::set_error(RT_ERR_UNSUPPORTED, "more than 8 Bvh::with_predictor BVHs");
     struct Part {
         const void* src;
         uint64_t bytes;
@@ -1687,6 +1821,8 @@ int rt_scene_upload(const rt_scene_desc* desc, int device, rt_scene_handle* out)
         {hs.perm.data(), hs.perm.size(), 0},
         {hs.texels.data(), hs.texels.size(), 0},
         {hs.nodes2.data(), hs.nodes2.size() * sizeof(f4), 0},
+        {hs.hrpp_keys.data(), hs.hrpp_keys.size() * sizeof(uint64_t), 0},
+        {hs.hrpp_vals.data(), hs.hrpp_vals.size() * sizeof(uint32_t), 0},
     };
     uint64_t total = 0;
     for (auto& p : parts) {
@@ -1734,6 +1870,11 @@ int rt_scene_upload(const rt_scene_desc* desc, int device, rt_scene_handle* out)
     d.stack_depth = hs.max_stack;
     s->stack_ref = hs.max_stack_ref;
     d.perm_bytes = (uint32_t)hs.perm.size();
+    d.hrpp_tab = nullptr;  // set per RT_FLAG_HRPP launch
+    d.hrpp_keys = (const unsigned long long*)(base + parts[12].off);
+    d.hrpp_vals = (const uint32_t*)(base + parts[13].off);
+    d.hrpp_nkeys = (uint32_t)hs.hrpp_keys.size();
+    d.hrpp_npred = hs.num_predictors;
     s->coord_bound = hs.coord_bound;
     uint64_t c[10] = {hs.entries.size(), hs.sph.size(), hs.msph.size() / 3, hs.rect.size() / 2, hs.tri.size() / 3,
                       hs.nodes.size() / rtdev::kBvhNodeF4, hs.mats.size(), hs.texs.size(), hs.max_bvh_depth, total};
@@ -1796,11 +1937,52 @@ int rt_scene_free(rt_scene_handle s) {
         if (s->sbuf) (void)hipFree(s->sbuf);
         if (s->counter) (void)hipFree(s->counter);
         if (s->replay) (void)hipFree(s->replay);
+        if (s->hrpp_tab) (void)hipFree(s->hrpp_tab);
+        if (s->hrpp_stats) (void)hipFree(s->hrpp_stats);
         for (int i = 0; i < rt_scene::kEvents; ++i)
             for (int j = 0; j < 2; ++j)
                 if (s->ev[i][j]) (void)hipEventDestroy(s->ev[i][j]);
     }
     delete s;
+    return RT_OK;
+}
+
+int rt_scene_hrpp_stats(rt_scene_handle s, uint64_t* out, uint32_t capacity, uint32_t* count) {
+    rthost::clear_error();
+    if (!s || !count) return rthost::set_error(RT_ERR_INVALID, "NULL argument");
+    const uint32_t np = s->dev.hrpp_npred;
+    *count = np;
+    if (!out || capacity < 6u * np) return capacity == 0 ? RT_OK : rthost::set_error(RT_ERR_INVALID, "capacity < 6 per predictor");
+    memset(out, 0, sizeof(uint64_t) * 6u * np);
+    if (!s->hrpp_stats) return RT_OK;  // no RT_FLAG_HRPP render yet
+    DeviceGuard g(s->device);
+    unsigned long long h[4 * rtdev::kHrppMaxPredictors] = {};
+    unsigned long long* d_tab_counts = nullptr;
+    hipError_t e;
+    if ((e = hipMalloc(&d_tab_counts, 16u * np)) != hipSuccess ||
+        (e = hipMemset(d_tab_counts, 0, 16u * np)) != hipSuccess) {
+        if (d_tab_counts) (void)hipFree(d_tab_counts);
+        return hip_fail(e, "HRPP stats");
+    }
+    (void)hipGetLastError();
+    if (s->hrpp_bits)
+        hipLaunchKernelGGL(hrpp_count, dim3(1024), dim3(256), 0, nullptr, s->hrpp_tab, s->hrpp_bits, np, d_tab_counts);
+    unsigned long long tc[2 * rtdev::kHrppMaxPredictors] = {};
+    if ((e = hipGetLastError()) != hipSuccess || (e = hipDeviceSynchronize()) != hipSuccess ||
+        (e = hipMemcpy(h, s->hrpp_stats, 32u * np, hipMemcpyDeviceToHost)) != hipSuccess ||
+        (e = hipMemcpy(tc, d_tab_counts, 16u * np, hipMemcpyDeviceToHost)) != hipSuccess) {
+        (void)hipFree(d_tab_counts);
+        return hip_fail(e, "HRPP stats");
+    }
+    (void)hipFree(d_tab_counts);
+    for (uint32_t p = 0; p < np; ++p) {
+        out[6 * p + 0] = h[4 * p + 0];
+        out[6 * p + 1] = h[4 * p + 1];
+        out[6 * p + 2] = h[4 * p + 2];
+        out[6 * p + 3] = tc[2 * p + 0];
+        out[6 * p + 4] = tc[2 * p + 1];
+        out[6 * p + 5] = h[4 * p + 3];
+    }
     return RT_OK;
 }
 
@@ -1887,13 +2069,38 @@ int rt_render_launch(rt_scene_handle s, const rt_camera_desc* camera, const rt_r
     dev_ref.stack_depth = s->stack_ref;
     const size_t perm_lds = s->dev.perm_bytes != 0u && s->dev.perm_bytes <= kPermLdsMax ? s->dev.perm_bytes : 0u;
     const size_t lds = (size_t)s->dev.stack_depth * 128u * sizeof(uint32_t) + perm_lds;
-    const size_t lds_ref = (size_t)dev_ref.stack_depth * 128u * sizeof(uint32_t) + perm_lds;
+    size_t lds_ref = (size_t)dev_ref.stack_depth * 128u * sizeof(uint32_t) + perm_lds;
+    if ((dp.flags & RT_FLAG_HRPP) && s->dev.hrpp_npred) {  // the experiment: reference kernel + predictors
+        dp.flags |= RT_FLAG_EXACT_BVH;
+        uint32_t bits = 22u;  // 4 M slots (128 MiB) per predictor
+        if (const char* env = getenv("RT_HRPP_SLOT_BITS")) bits = (uint32_t)strtoul(env, nullptr, 10);
+        if (bits > 28u) bits = 28u;
+        const uint64_t bytes = bits ? ((uint64_t)s->dev.hrpp_npred << bits) * sizeof(rtdev::HrppSlot) : 0u;
+        if (s->hrpp_tab_bytes < bytes || !s->hrpp_stats) {
+            if (s->hrpp_tab) (void)hipFree(s->hrpp_tab);
+            s->hrpp_tab = nullptr;
+            s->hrpp_tab_bytes = 0;
+            if ((e = hipMalloc(&s->hrpp_tab, bytes ? bytes : sizeof(rtdev::HrppSlot))) != hipSuccess ||
+                (!s->hrpp_stats && (e = hipMalloc(&s->hrpp_stats, 8u * 4u * rtdev::kHrppMaxPredictors)) != hipSuccess))
+                return rthost::set_error(RT_ERR_OOM, std::string("hipMalloc HRPP tables: ") + hipGetErrorString(e));
+            s->hrpp_tab_bytes = bytes;
+        }
+        s->hrpp_bits = bits;
+        if ((bytes && (e = hipMemsetAsync(s->hrpp_tab, 0xff, bytes, (hipStream_t)stream)) != hipSuccess) ||
+            (e = hipMemsetAsync(s->hrpp_stats, 0, 8u * 4u * rtdev::kHrppMaxPredictors, (hipStream_t)stream)) !=
+                hipSuccess)
+            return hip_fail(e, "HRPP table reset");
+        dev_ref.hrpp_tab = s->hrpp_tab;
+        dev_ref.hrpp_stats = s->hrpp_stats;
+        dev_ref.hrpp_bits = bits;
+        lds_ref += 4u * rtdev::kHrppMaxPredictors * sizeof(uint32_t);
+    }
     if (s->grid == 0) {
         int per_cu = 0, per_cu_ref = 0, cus = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace_samples<false>, 64, lds) != hipSuccess ||
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace_samples<0>, 64, lds) != hipSuccess ||
             per_cu < 1)
             per_cu = 8;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_ref, trace_samples<true>, 64, lds_ref) != hipSuccess ||
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_ref, trace_samples<1>, 64, lds_ref) != hipSuccess ||
             per_cu_ref < 1)
             per_cu_ref = 8;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s->device) != hipSuccess || cus < 1)
@@ -1925,13 +2132,16 @@ int rt_render_launch(rt_scene_handle s, const rt_camera_desc* camera, const rt_r
         }
         if (evp) (void)hipEventRecord(evp[0], st);
         (void)hipGetLastError();  // hipGetLastError is sticky: drop an unrelated earlier error
-        if (exact) {  // every BVH traversed by the literal replay of bvh.rs
-            hipLaunchKernelGGL(trace_samples<true>, dim3(grid_ref), dim3(64), lds_ref, st, dev_ref, cam, dp, q,
+        if (dev_ref.hrpp_tab) {  // RT_FLAG_HRPP: the reference kernel with predictors
+            hipLaunchKernelGGL(trace_samples<2>, dim3(grid_ref), dim3(64), lds_ref, st, dev_ref, cam, dp, q,
+                               s->sbuf, s->counter, s->replay, 0u, d_segments);
+        } else if (exact) {  // every BVH traversed by the literal replay of bvh.rs
+            hipLaunchKernelGGL(trace_samples<1>, dim3(grid_ref), dim3(64), lds_ref, st, dev_ref, cam, dp, q,
                                s->sbuf, s->counter, s->replay, 0u, d_segments);
         } else {  // fast kernel, then the reference kernel on the samples it handed over
-            hipLaunchKernelGGL(trace_samples<false>, dim3(grid), dim3(64), lds, st, s->dev, cam, dp, q, s->sbuf,
+            hipLaunchKernelGGL(trace_samples<0>, dim3(grid), dim3(64), lds, st, s->dev, cam, dp, q, s->sbuf,
                                s->counter, s->replay, 0u, d_segments);
-            hipLaunchKernelGGL(trace_samples<true>, dim3(grid_ref), dim3(64), lds_ref, st, dev_ref, cam, dp, q,
+            hipLaunchKernelGGL(trace_samples<1>, dim3(grid_ref), dim3(64), lds_ref, st, dev_ref, cam, dp, q,
                                s->sbuf, s->counter, s->replay, 1u, d_segments);
         }
         if ((e = hipGetLastError()) != hipSuccess) return hip_fail(e, "trace_samples launch");

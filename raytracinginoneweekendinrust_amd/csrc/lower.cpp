@@ -30,7 +30,7 @@ uint64_t HostScene::bytes() const {
     return entries.size() * sizeof(rtdev::DevEntry) + sph.size() * 16 + sph_mat.size() * 4 +
            msph.size() * 16 + rect.size() * 16 + tri.size() * 16 + nodes.size() * 16 + nodes2.size() * 16 +
            mats.size() * sizeof(rtdev::DevMaterial) + texs.size() * sizeof(rtdev::DevTexture) +
-           perm.size() + texels.size();
+           perm.size() + texels.size() + hrpp_keys.size() * 8 + hrpp_vals.size() * 4;
 }
 
 // ---------------------------------------------------------------------------
@@ -723,6 +723,34 @@ class Lowerer {
         // its rank[3] carries the BVH's flags
         put(base, {Slot{true, wroot | 0x40000000u, tn[troot].box, 0u}}, prunable ? rtdev::kBvhPrunable : 0u);
         s_->nodes[(size_t)base * rtdev::kBvhNodeF4 + 7].z = bitsf(base2);  // wrapper rank[2]: the BVH2 wrapper
+        if (n.ref[1] == 1) {  // Bvh::with_predictor (bvh.rs:69-80): HRPP side data
+            // The predictor table stores, per ray hash, "leaf nodes" (GO_UP_LEVEL = 0,
+            // bvh.rs:22: the BvhNode whose child object was hit). Each gets a
+            // wrapper-format record (its own box, child 0 = the node) so that
+            // nodes[p].hit(...) is bvh_hit_reference from that record, and every
+            // leaf code maps to it (cube faces too: a cube hit reports its face).
+            const uint32_t pid = ++s_->num_predictors;
+            s_->nodes2[4 * (size_t)base2 + 3].z = bitsf(pid);
+            for (uint32_t i = 0; i < tn.size(); ++i) {
+                if (tn[i].is_node[0] || tn[i].is_node[1]) continue;
+                const uint32_t w = (uint32_t)(s_->nodes2.size() / 4);
+                if (w > rtdev::kMaxIndex) return fail(RT_ERR_UNSUPPORTED, "too many BVH nodes");
+                s_->nodes2.resize(s_->nodes2.size() + 4);
+                put2(w, tn[i].box, none2, remap2[i], rtdev::kChildEmpty);
+                for (int k = 0; k < 2; ++k) {
+                    const uint32_t c = tn[i].child[k];
+                    if (c == rtdev::kChildEmpty) continue;
+                    s_->hrpp_keys.push_back((uint64_t)base2 << 32 | c);
+                    s_->hrpp_vals.push_back(w);
+                    if (rtdev::leaf_type(c) == rtdev::kLeafCube)
+                        for (uint32_t f = 0; f < 6u; ++f) {
+                            s_->hrpp_keys.push_back((uint64_t)base2 << 32 |
+                                                    rtdev::leaf_code(rtdev::kLeafRect, rtdev::leaf_index(c) + f));
+                            s_->hrpp_vals.push_back(w);
+                        }
+                }
+            }
+        }
         uint32_t max_wide_depth = 0;
         for (uint32_t w = 0; w < wide.size(); ++w) {
             put(base + 1 + w, wide[w], 0u);
@@ -853,6 +881,19 @@ int lower_scene(const rt_scene_desc* desc, HostScene* out, std::string* err, con
     *out = HostScene();
     Lowerer l(desc, out, err, orderer);
     int rc = l.run();
+    {  // HRPP leaf map sorted by key (binary search on the device)
+        std::vector<uint32_t> idx(out->hrpp_keys.size());
+        for (uint32_t i = 0; i < idx.size(); ++i) idx[i] = i;
+        std::sort(idx.begin(), idx.end(), [&](uint32_t a, uint32_t b) { return out->hrpp_keys[a] < out->hrpp_keys[b]; });
+        std::vector<uint64_t> k(idx.size());
+        std::vector<uint32_t> v(idx.size());
+        for (uint32_t i = 0; i < idx.size(); ++i) {
+            k[i] = out->hrpp_keys[idx[i]];
+            v[i] = out->hrpp_vals[idx[i]];
+        }
+        out->hrpp_keys.swap(k);
+        out->hrpp_vals.swap(v);
+    }
     out->coord_bound += l.translate_sum();
     return rc;
 }

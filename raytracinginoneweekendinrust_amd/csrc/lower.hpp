@@ -27,6 +27,11 @@ struct HostScene {
     // Upper bound on |coordinate| of any primitive in any instance frame plus the
     // translations applied to reach it (bounds ray lengths for the pruning margin).
     float coord_bound = 0.0f;
+    // HRPP (Bvh::with_predictor BVHs): count, and the sorted map
+    // (BVH2 wrapper << 32 | leaf code) -> wrapper-format record of its leaf node.
+    uint32_t num_predictors = 0;
+    std::vector<uint64_t> hrpp_keys;
+    std::vector<uint32_t> hrpp_vals;
     uint64_t bytes() const;
 };
 

@@ -62,7 +62,8 @@ class SceneBuilder {
     int cube(Vec3 mn, Vec3 mx, int mat);
     int tri(Vec3 p0, Vec3 p1, Vec3 p2, int mat);
     int list(const HittableList& l);
-    int bvh(const HittableList& l, float t0, float t1, uint64_t axis_seed);
+    // predictor: Bvh::with_predictor (bvh.rs:69-80) rather than Bvh::new
+    int bvh(const HittableList& l, float t0, float t1, uint64_t axis_seed, bool predictor = false);
     int translate(int child, Vec3 d);
     int rotate_y(int child, float degrees);
     int constant_medium(int boundary, float density, int tex);

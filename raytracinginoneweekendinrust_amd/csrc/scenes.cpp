@@ -7,8 +7,9 @@
 // gen_range). Each BVH gets its split-axis stream seed from this stream at the
 // point where the reference calls Bvh::new / Bvh::with_predictor.
 //
-// HRPP predictors (Bvh::with_predictor, src/main.rs:586, 679, 824) are not
-// built: the device path always uses the exact traversal (bvh.rs:212-217).
+// HRPP predictors (Bvh::with_predictor, src/main.rs:586, 679, 824) are marked
+// on their BVH nodes (ref[1] = 1); renders use the exact traversal (bvh.rs:212-217)
+// unless RT_FLAG_HRPP asks for the prediction experiment.
 #include <math.h>
 #include <stddef.h>
 #include <stdlib.h>
@@ -120,9 +121,9 @@ int SceneBuilder::list(const HittableList& l) {
     items.insert(items.end(), l.objects.begin(), l.objects.end());
     return add(RT_OBJ_LIST, {}, first, (int)l.objects.size());
 }
-int SceneBuilder::bvh(const HittableList& l, float t0, float t1, uint64_t axis_seed) {
+int SceneBuilder::bvh(const HittableList& l, float t0, float t1, uint64_t axis_seed, bool predictor) {
     int li = list(l);
-    return add(RT_OBJ_BVH, {t0, t1}, li, -1, -1, axis_seed);
+    return add(RT_OBJ_BVH, {t0, t1}, li, predictor ? 1 : -1, -1, axis_seed);
 }
 int SceneBuilder::translate(int child, Vec3 d) { return add(RT_OBJ_TRANSLATE, {d.x, d.y, d.z}, child); }
 int SceneBuilder::rotate_y(int child, float degrees) { return add(RT_OBJ_ROTATE_Y, {degrees}, child); }
@@ -332,7 +333,7 @@ int cornell(SceneBuilder& b, bool smoke, int* world) {
     return RT_OK;
 }
 
-// src/main.rs:559-686 (HRPP predictors not built; exact traversal)
+// src/main.rs:559-686 (both BVHs carry predictors, used only under RT_FLAG_HRPP)
 int showcase(SceneBuilder& b, SceneRng& rng, const std::string& dir, int* world) {
     HittableList boxes;
     int ground = b.lambertian_from_color(vec3(0.48f, 0.83f, 0.53f));
@@ -350,7 +351,7 @@ int showcase(SceneBuilder& b, SceneRng& rng, const std::string& dir, int* world)
         }
     }
     HittableList wl;
-    wl.add(b.bvh(boxes, 0.0f, 1.0f, rng.next_u64()));
+    wl.add(b.bvh(boxes, 0.0f, 1.0f, rng.next_u64(), true));  // Bvh::with_predictor, main.rs:586-591
     int light = b.diffuse_light_from_color(vec3(7.0f, 7.0f, 7.0f));
     wl.add(b.xz_rect(123.0f, 423.0f, 147.0f, 412.0f, 554.0f, light));
     Vec3 center1 = vec3(400.0f, 400.0f, 200.0f);
@@ -379,7 +380,7 @@ int showcase(SceneBuilder& b, SceneRng& rng, const std::string& dir, int* world)
         float rz = rng.range(0.0f, max_val);
         spheres.add(b.sphere(vec3(rx, ry, rz), 10.0f, white));
     }
-    int sb = b.bvh(spheres, 0.0f, 1.0f, rng.next_u64());
+    int sb = b.bvh(spheres, 0.0f, 1.0f, rng.next_u64(), true);  // main.rs:679
     wl.add(b.translate(b.rotate_y(sb, 15.0f), vec3(-100.0f, 270.0f, 395.0f)));
     *world = b.list(wl);
     return RT_OK;
@@ -498,6 +499,7 @@ int load_obj_tris(const std::string& path, std::vector<float>* out) {
 
 // src/main.rs:791-829 (bunny / gargoyle / igea_hrpp)
 int mesh_scene(SceneBuilder& b, SceneRng& rng, const std::string& dir, const char* file, Vec3 disp, bool synthetic_ok,
+               bool predictor,
                int* world) {
     HittableList w = cornell_boundaries(b);
     int white = b.lambertian_from_color(vec3(0.73f, 0.73f, 0.73f));
@@ -513,7 +515,7 @@ int mesh_scene(SceneBuilder& b, SceneRng& rng, const std::string& dir, const cha
     for (size_t i = 0; i + 8 < tris.size(); i += 9)
         mesh.add(b.tri(vec3(tris[i], tris[i + 1], tris[i + 2]), vec3(tris[i + 3], tris[i + 4], tris[i + 5]),
                        vec3(tris[i + 6], tris[i + 7], tris[i + 8]), white));
-    int bvh = b.bvh(mesh, 0.0f, 1.0f, rng.next_u64());
+    int bvh = b.bvh(mesh, 0.0f, 1.0f, rng.next_u64(), predictor);  // igea: Bvh::with_predictor, main.rs:824
     w.add(b.translate(bvh, disp));
     *world = b.list(w);
     return RT_OK;
@@ -535,9 +537,9 @@ int generate_scene(const std::string& name, uint64_t seed, const std::string& as
     else if (name == "cornell") rc = cornell(b, false, &world);
     else if (name == "cornell-smoke") rc = cornell(b, true, &world);
     else if (name == "showcase") rc = showcase(b, rng, asset_dir, &world);
-    else if (name == "bunny") rc = mesh_scene(b, rng, asset_dir, "bunny_2000_scale.obj", vec3(325.0f, 0.0f, 200.0f), true, &world);
-    else if (name == "gargoyle") rc = mesh_scene(b, rng, asset_dir, "gargoyle.obj", vec3(275.0f, 0.0f, 200.0f), false, &world);
-    else if (name == "igea-hrpp") rc = mesh_scene(b, rng, asset_dir, "igea.obj", vec3(275.0f, 0.0f, 200.0f), false, &world);
+    else if (name == "bunny") rc = mesh_scene(b, rng, asset_dir, "bunny_2000_scale.obj", vec3(325.0f, 0.0f, 200.0f), true, false, &world);
+    else if (name == "gargoyle") rc = mesh_scene(b, rng, asset_dir, "gargoyle.obj", vec3(275.0f, 0.0f, 200.0f), false, false, &world);
+    else if (name == "igea-hrpp") rc = mesh_scene(b, rng, asset_dir, "igea.obj", vec3(275.0f, 0.0f, 200.0f), false, true, &world);
     else return set_error(RT_ERR_INVALID, "unknown scene '" + name + "'");
     if (rc) return rc;
     *out = b.finish(world);

@@ -43,6 +43,8 @@ def test_showcase_structure(rt):
     y1 = cubes["f"][:, 4]
     assert np.all((y1 >= 1.0) & (y1 < 101.0))
     assert count(n, K.RT_OBJ_BVH) == 2
+    bvh = n[n["kind"] == K.RT_OBJ_BVH]
+    assert np.all(bvh["ref"][:, 1] == 1)  # both are Bvh::with_predictor (main.rs:586-591, 679)
     assert count(n, K.RT_OBJ_CONSTANT_MEDIUM) == 2
     assert count(n, K.RT_OBJ_MOVING_SPHERE) == 1
     assert count(n, K.RT_TEX_IMAGE) == 1 and count(n, K.RT_TEX_MARBLE) == 1
@@ -55,6 +57,7 @@ def test_bunny_substitute_mesh(rt):
     n = rt.Scene.generate("bunny", 20231).nodes()
     tris = n[n["kind"] == K.RT_OBJ_TRI]
     assert len(tris) == 20480
+    assert np.all(n[n["kind"] == K.RT_OBJ_BVH]["ref"][:, 1] == -1)  # bunny: Bvh::new (main.rs:797)
     ys = tris["f"][:, [1, 4, 7]]
     assert ys.min() >= 0.0 and ys.max() < 300
 

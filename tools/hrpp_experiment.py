@@ -1,0 +1,70 @@
+#!/usr/bin/env python3
+"""HRPP experiment (src/hrpp.rs, src/bvh.rs:114-211), reported apart
+from the parity path: the same frame rendered with the exact reference traversal
+(RT_FLAG_EXACT_BVH, trace_samples<1>), with HRPP predictors on both showcase BVHs
+(RT_FLAG_HRPP, trace_samples<2>: the same kernel plus prediction), and with the fast
+BVH4 path (the product). Prints one JSON line: device times, predictor statistics,
+and the image error HRPP introduces relative to the exact render.
+
+    python3 tools/hrpp_experiment.py [--config C3] [--width 1200] [--spp 500] [--bits 22]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+import raytracinginoneweekendinrust_amd as rt  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="C3")
+    ap.add_argument("--width", type=int, default=0)
+    ap.add_argument("--spp", type=int, default=0)
+    ap.add_argument("--bits", type=int, default=22)
+    a = ap.parse_args()
+    base = rt.CONFIGS[a.config]
+    cfg = base.scaled(a.width or base.width, a.spp or base.spp)
+    os.environ["RT_HRPP_SLOT_BITS"] = str(a.bits)
+    scene = rt.Scene.generate(cfg.scene, cfg.scene_seed)
+    ds = rt.DeviceScene(scene)
+    out = {"config": cfg.name, "width": cfg.width, "height": cfg.height, "spp": cfg.spp, "slot_bits": a.bits}
+    imgs = {}
+    for name, kw in (("fast", {}), ("exact", {"exact_bvh": True}), ("hrpp", {"hrpp": True})):
+        p = rt.render_params(cfg.width, cfg.height, cfg.spp, cfg.depth, background=cfg.background(), **kw)
+        ds.render(cfg.camera(), p)  # warm-up (and table allocation)
+        ds.trace_time(reset=True)
+        t0 = time.perf_counter()
+        img, st = ds.render(cfg.camera(), p)
+        wall = time.perf_counter() - t0
+        ms, _ = ds.trace_time(reset=True)
+        imgs[name] = img
+        out[name] = {"trace_ms": round(ms, 2), "wall_s": round(wall, 3),
+                     "msamples_per_s": round(cfg.samples / (ms * 1e3), 1), "segments": st["segments"]}
+        if name == "hrpp":
+            out["predictors"] = ds.hrpp_stats()
+    ds.close()
+    e, h = np.clip(imgs["exact"], 0, 1), np.clip(imgs["hrpp"], 0, 1)
+    q = lambda x: np.floor(x * 255 + 0.5).astype(np.int32)  # palette f32 -> u8 on clamp01
+    out["hrpp_vs_exact"] = {
+        "mean_abs": float(np.abs(h - e).mean()), "rmse": float(np.sqrt(((h - e) ** 2).mean())),
+        "max_abs": float(np.abs(h - e).max()),
+        "u8_pixels_differing": float((q(h) != q(e)).any(axis=2).mean()),
+        "mean_luminance_exact": float(e.mean()), "mean_luminance_hrpp": float(h.mean()),
+    }
+    for s in out["predictors"]:
+        calls = s["true_positive"] + s["false_positive"] + s["no_prediction"]
+        s["calls"] = calls
+        for k in ("true_positive", "false_positive", "no_prediction"):
+            s["ratio_" + k] = round(s[k] / max(calls, 1), 4)
+    out["speedup_hrpp_vs_exact"] = round(out["exact"]["trace_ms"] / out["hrpp"]["trace_ms"], 3)
+    out["speedup_fast_vs_hrpp"] = round(out["hrpp"]["trace_ms"] / out["fast"]["trace_ms"], 3)
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
