@@ -64,6 +64,16 @@ enum ProfRegion : uint32_t {
 // traversal mode bits (bvh_hit): kModeExact = RT_FLAG_EXACT_BVH; the rest come
 // from DevParams::tune (RT_TUNE environment variable, diagnostics / A-B runs).
 constexpr uint32_t kModeExact = 1u, kModeNoLeafBoxes = 2u;
+#ifdef RT_ABLATE
+// Ablation build (librtamd_ablate.so, diagnostics only): RT_TUNE bits that run a
+// piece of work twice (results of the copy discarded through an opaque test),
+// so the time delta prices that work without changing any path.
+constexpr uint32_t kAbLeaf2 = 1u << 8, kAbKeys2 = 1u << 9, kAbBvh2 = 1u << 10, kAbMedium2 = 1u << 11,
+                   kAbGeom2 = 1u << 12;
+#define ABLATE(bit, ...) do { if (mode & (bit)) { __VA_ARGS__ } } while (0)
+#else
+#define ABLATE(bit, ...) do { } while (0)
+#endif
 #ifdef RT_PROFILE_REGIONS
 constexpr uint32_t kProfCopies = 64;  // flush targets spread over blockIdx to keep atomics uncontended
 constexpr uint32_t kProfWords = 3 * kPrCount + 16;  // region triples, then the two visit histograms
@@ -345,6 +355,18 @@ RT_DEV void rect_axes(uint32_t axis, const Ray& r, float& ok, float& dk, float& 
     ob = sel3(axis, oy, oz, oz);
     db = sel3(axis, dy, dz, dz);
 }
+// rectangle.rs:36-65 with the plane axis resolved: k along (ok, dk), bounds
+// [a0, a1] x [b0, b1] along (oa, da) x (ob, db). Same IEEE operations as rect_t.
+RT_DEV bool side_t(float k, float ok, float dk, float oa, float da, float ob, float db, float a0, float a1, float b0,
+                   float b1, float tmin, float tmax, float& t) {
+    const float tt = (k - ok) / dk;
+    if (tt < tmin || tt > tmax) return false;
+    const float x = oa + tt * da;
+    const float y = ob + tt * db;
+    if (x < a0 || x > a1 || y < b0 || y > b1) return false;
+    t = tt;
+    return true;
+}
 RT_DEV bool rect_t(f4 r0, f4 r1, const Ray& r, float tmin, float tmax, float& t) {
     float ok, dk, oa, da, ob, db;
     rect_axes(__float_as_uint(r1.y), r, ok, dk, oa, da, ob, db);
@@ -401,15 +423,22 @@ RT_DEV bool leaf_hit(const DevScene& S, uint32_t code, const Ray& r, const RayD&
         return false;
     }
     if (type == rtdev::kLeafCube) {  // cube.rs:84-93: the six sides as a HittableList
+        // The sides' axes are fixed (cube.rs:25-74: xy z0, xy z1, xz y0, xz y1,
+        // yz x0, yz x1) and their bounds are the box's six values, read from the
+        // records of sides 0 and 2: (z0, x0, x1, y0), y1 and (y0, x0, x1, z0), z1.
+        const f4 s0 = ld4(S.rect + 2 * idx), s2 = ld4(S.rect + 2 * idx + 4);
+        const float y1 = ld2(S.rect + 2 * idx + 1, 0).x, z1 = ld2(S.rect + 2 * idx + 5, 0).x;
+        const float x0 = s0.y, x1 = s0.z, y0 = s0.w, z0 = s0.x;
+        const float ox = r.o.x, oy = r.o.y, oz = r.o.z, dx = r.d.x, dy = r.d.y, dz = r.d.z;
         bool any = false;
-        for (uint32_t i = 0; i < 6u; ++i) {
-            uint32_t ri = idx + i;
-            if (rect_t(ld4(S.rect + 2 * ri), ld4(S.rect + 2 * ri + 1), r, tmin, closest, t)) {
-                closest = t;
-                hit_code = rtdev::leaf_code(rtdev::kLeafRect, ri);
-                any = true;
-            }
-        }
+        uint32_t face = 0u;
+        if (side_t(z0, oz, dz, ox, dx, oy, dy, x0, x1, y0, y1, tmin, closest, t)) { closest = t; face = 0u; any = true; }
+        if (side_t(z1, oz, dz, ox, dx, oy, dy, x0, x1, y0, y1, tmin, closest, t)) { closest = t; face = 1u; any = true; }
+        if (side_t(y0, oy, dy, ox, dx, oz, dz, x0, x1, z0, z1, tmin, closest, t)) { closest = t; face = 2u; any = true; }
+        if (side_t(y1, oy, dy, ox, dx, oz, dz, x0, x1, z0, z1, tmin, closest, t)) { closest = t; face = 3u; any = true; }
+        if (side_t(x0, ox, dx, oy, dy, oz, dz, y0, y1, z0, z1, tmin, closest, t)) { closest = t; face = 4u; any = true; }
+        if (side_t(x1, ox, dx, oy, dy, oz, dz, y0, y1, z0, z1, tmin, closest, t)) { closest = t; face = 5u; any = true; }
+        if (any) hit_code = rtdev::leaf_code(rtdev::kLeafRect, idx + face);
         return any;
     }
     if (type == rtdev::kLeafTri) {
@@ -530,7 +559,7 @@ RT_DEV bool leaf_box_may_hit(float x0, float y0, float z0, float x1, float y1, f
     do {                                                                                               \
         float c_ = tmax_entry;                                                                         \
         uint32_t hc_ = 0u;                                                                             \
-        if (leaf_hit(S, (CODE_), r, q, tmin, c_, hc_) && !(c_ > bound)) {                              \
+        if (leaf_hit(S, (CODE_), r, to_d(r), tmin, c_, hc_) && !(c_ > bound)) {                              \
             unsigned i_ = atomicAdd(&g_audit_count, 1u);                                               \
             if (i_ < kAuditMax) {                                                                      \
                 LeafAudit& A = g_audit[i_];                                                            \
@@ -779,8 +808,8 @@ RT_DEV bool bvh_hit(const DevScene& S, float delta, uint32_t root, const Ray& r,
     const float tmax_entry = closest;
     const f4* wrapper = S.nodes + (size_t)root * rtdev::kBvhNodeF4;
     const V inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
-    const RayD q = to_d(r);
     if constexpr (kKind != 0) {
+        const RayD q = to_d(r);
         const uint32_t w2 = __float_as_uint(wrapper[7].z);
         if constexpr (kKind == 2) {
             const uint32_t pid = __float_as_uint(S.nodes2[4 * (size_t)w2 + 3].z);
@@ -840,6 +869,9 @@ RT_DEV bool bvh_hit(const DevScene& S, float delta, uint32_t root, const Ray& r,
                     const float cap = closest < kInf ? __uint_as_float(__float_as_uint(closest) + 1u) : kInf;
                     float c = tmr < cap ? tmr : cap;
                     uint32_t code = 0u;
+                    const RayD q = to_d(r);  // f64 ray for sphere leaves, rebuilt here rather than kept live
+                    ABLATE(kAbLeaf2, float c2 = c; uint32_t h2 = 0u;
+                           if (leaf_hit(S, lcode, r, q, tmin, c2, h2) && h2 == 0x7fffffffu) c = -1.0f;);
                     if (leaf_hit(S, lcode, r, q, tmin, c, code)) {
                         // cube faces rank + 0..5 (the face leaf_hit's list walk kept)
                         const uint32_t rk = rank + (rtdev::leaf_type(lcode) == rtdev::kLeafCube
@@ -875,18 +907,46 @@ RT_DEV bool bvh_hit(const DevScene& S, float delta, uint32_t root, const Ray& r,
             c1 = __float_as_uint(chf.y);
             c2 = __float_as_uint(chf.z);
             c3 = __float_as_uint(chf.w);
-            if (c0 != rtdev::kChildEmpty)
-                t0 = child_key(mnx.x, mny.x, mnz.x, mxx.x, mxy.x, mxz.x, r, inv, tmin, tmax_entry, closest, prune,
-                               delta);
-            if (c1 != rtdev::kChildEmpty)
-                t1 = child_key(mnx.y, mny.y, mnz.y, mxx.y, mxy.y, mxz.y, r, inv, tmin, tmax_entry, closest, prune,
-                               delta);
-            if (c2 != rtdev::kChildEmpty)
-                t2 = child_key(mnx.z, mny.z, mnz.z, mxx.z, mxy.z, mxz.z, r, inv, tmin, tmax_entry, closest, prune,
-                               delta);
-            if (c3 != rtdev::kChildEmpty)
-                t3 = child_key(mnx.w, mny.w, mnz.w, mxx.w, mxy.w, mxz.w, r, inv, tmin, tmax_entry, closest, prune,
-                               delta);
+            // The inflated-entry pass can only prune once closest is finite
+            // (prune_bound(inf) = inf); while no active lane has a hit yet, the
+            // whole wave skips it.
+            const bool prune_now = prune && closest < kInf;
+            ABLATE(kAbKeys2, float k2 = child_key(mnx.x, mny.x, mnz.x, mxx.x, mxy.x, mxz.x, r, inv, tmin, tmax_entry,
+                                                  closest, prune_now, delta) +
+                                        child_key(mnx.y, mny.y, mnz.y, mxx.y, mxy.y, mxz.y, r, inv, tmin, tmax_entry,
+                                                  closest, prune_now, delta) +
+                                        child_key(mnx.z, mny.z, mnz.z, mxx.z, mxy.z, mxz.z, r, inv, tmin, tmax_entry,
+                                                  closest, prune_now, delta) +
+                                        child_key(mnx.w, mny.w, mnz.w, mxx.w, mxy.w, mxz.w, r, inv, tmin, tmax_entry,
+                                                  closest, prune_now, delta);
+                   if (k2 == -1.0f) c0 = 0u;);
+            if (__ballot(prune_now) != 0ull) {
+                if (c0 != rtdev::kChildEmpty)
+                    t0 = child_key(mnx.x, mny.x, mnz.x, mxx.x, mxy.x, mxz.x, r, inv, tmin, tmax_entry, closest,
+                                   prune_now, delta);
+                if (c1 != rtdev::kChildEmpty)
+                    t1 = child_key(mnx.y, mny.y, mnz.y, mxx.y, mxy.y, mxz.y, r, inv, tmin, tmax_entry, closest,
+                                   prune_now, delta);
+                if (c2 != rtdev::kChildEmpty)
+                    t2 = child_key(mnx.z, mny.z, mnz.z, mxx.z, mxy.z, mxz.z, r, inv, tmin, tmax_entry, closest,
+                                   prune_now, delta);
+                if (c3 != rtdev::kChildEmpty)
+                    t3 = child_key(mnx.w, mny.w, mnz.w, mxx.w, mxy.w, mxz.w, r, inv, tmin, tmax_entry, closest,
+                                   prune_now, delta);
+            } else {
+                if (c0 != rtdev::kChildEmpty)
+                    t0 = child_key(mnx.x, mny.x, mnz.x, mxx.x, mxy.x, mxz.x, r, inv, tmin, tmax_entry, closest, false,
+                                   delta);
+                if (c1 != rtdev::kChildEmpty)
+                    t1 = child_key(mnx.y, mny.y, mnz.y, mxx.y, mxy.y, mxz.y, r, inv, tmin, tmax_entry, closest, false,
+                                   delta);
+                if (c2 != rtdev::kChildEmpty)
+                    t2 = child_key(mnx.z, mny.z, mnz.z, mxx.z, mxy.z, mxz.z, r, inv, tmin, tmax_entry, closest, false,
+                                   delta);
+                if (c3 != rtdev::kChildEmpty)
+                    t3 = child_key(mnx.w, mny.w, mnz.w, mxx.w, mxy.w, mxz.w, r, inv, tmin, tmax_entry, closest, false,
+                                   delta);
+            }
         }
         PROF_ADD(kPrBvhTrip, pt);
         PROF_T0(pp);
@@ -952,7 +1012,7 @@ RT_DEV bool bvh_hit(const DevScene& S, float delta, uint32_t root, const Ray& r,
     {  // the replay of the reference recursion must agree with the fast traversal
         float c2 = tmax_entry;
         uint32_t h2 = 0u;
-        bool a2 = bvh_hit_reference(S, __float_as_uint(wrapper[7].z), r, q, inv, tmin, c2, h2, stk);
+        bool a2 = bvh_hit_reference(S, __float_as_uint(wrapper[7].z), r, to_d(r), inv, tmin, c2, h2, stk);
         bool same = a2 == any && (!any || (__float_as_uint(c2) == __float_as_uint(closest) && h2 == hit_code));
         if (!same) {
             unsigned i_ = atomicAdd(&g_trav_audit_count, 1u);
@@ -989,9 +1049,15 @@ RT_DEV bool entry_geom_hit(const DevScene& S, float delta, const DevEntry* E, Ra
                            uint32_t& hit_code, uint32_t* stk, uint32_t mode, bool& replay) {
     uint32_t ntf = E->ntf;
     for (uint32_t i = 0; i < ntf; ++i) r = apply_op(E->tf[i], r);
-    if (E->kind == rtdev::kEntBvh)
+    if (E->kind == rtdev::kEntBvh) {
+        ABLATE(kAbBvh2, float c2 = closest; uint32_t h2 = 0u; bool rp = false;
+               if (bvh_hit<kKind>(S, delta, E->payload, r, tmin, c2, h2, stk, mode, rp) && h2 == 0x7fffffffu)
+                   closest = -1.0f;);
         return bvh_hit<kKind>(S, delta, E->payload, r, tmin, closest, hit_code, stk, mode, replay);
+    }
     RayD q = to_d(r);
+    ABLATE(kAbGeom2, float c2 = closest; uint32_t h2 = 0u;
+           if (leaf_hit(S, E->payload, r, q, tmin, c2, h2) && h2 == 0x7fffffffu) closest = -1.0f;);
     return leaf_hit(S, E->payload, r, q, tmin, closest, hit_code);
 }
 
@@ -1011,6 +1077,8 @@ RT_DEV bool medium_hit(const DevScene& S, float delta, const DevEntry* E, Ray r,
         uint32_t bn = B->ntf;
         for (uint32_t i = 0; i < bn; ++i) rb = apply_op(B->tf[i], rb);
         Roots R = sphere_roots(ld4(S.sph + rtdev::leaf_index(B->payload)), to_d(rb));
+        ABLATE(kAbMedium2, Roots R2 = sphere_roots(ld4(S.sph + rtdev::leaf_index(B->payload)), to_d(rb));
+               if (R2.r1 == -1.0) t1 = -1.0f;);
         if (!sphere_select(R, -kInf, kInf, t1)) return false;
         if (!sphere_select(R, t1 + 0.0001f, kInf, t2)) return false;
     } else {
