@@ -491,18 +491,6 @@ RT_DEV bool slab(float x0, float y0, float z0, float x1, float y1, float z1, con
     return !(t_max < t_min);
 }
 
-// Entry parameter of the ray into a box inflated by `delta` on every side (the
-// near-side half of the slab test above, on outward-rounded bounds).
-RT_DEV float slab_entry_inflated(float x0, float y0, float z0, float x1, float y1, float z1, const Ray& r, V inv,
-                                 float t_min, float delta) {
-    float ax = (inv.x < 0.0f ? (x1 + delta) - r.o.x : (x0 - delta) - r.o.x) * inv.x;
-    float ay = (inv.y < 0.0f ? (y1 + delta) - r.o.y : (y0 - delta) - r.o.y) * inv.y;
-    float az = (inv.z < 0.0f ? (z1 + delta) - r.o.z : (z0 - delta) - r.o.z) * inv.z;
-    t_min = ax > t_min ? ax : t_min;
-    t_min = ay > t_min ? ay : t_min;
-    t_min = az > t_min ? az : t_min;
-    return t_min;
-}
 // A subtree may be skipped once its inflated entry exceeds this bound: every
 // candidate inside it would then compute t > closest (exact pruning).
 RT_DEV float prune_bound(float closest) { return closest + __builtin_fabsf(closest) * 0x1p-19f; }
@@ -778,14 +766,21 @@ RT_DEV bool bvh_hit_hrpp(const DevScene& S, uint32_t wrapper2, uint32_t pid, con
 // One interior child of a BVH4 node: the reference's box test (stored box, the
 // t_max the BVH was entered with) and, when pruning, the inflated-entry bound.
 // Returns the sort key: the entry distance, +inf when the child is not visited.
+// The inflated entry is bounded from the reference test's own entry: along axis
+// a the delta shell is delta * |inv_a| thick in t, so entry(box + delta) >=
+// entry(box) - delta * max_a |inv_a| (= te - dmi). The gap to any candidate in
+// the box stays >= delta / |d|, which dominates the slab roundings exactly as in
+// the direct computation (exact pruning); a large dmi only weakens
+// the bound (no pruning), never strengthens it.
+// The returned key is what the stack keeps for the pop-time prune, so for a
+// prunable BVH it is always the conservative (inflated) entry, also while
+// closest is still infinite.
 RT_DEV float child_key(float x0, float y0, float z0, float x1, float y1, float z1, const Ray& r, V inv, float tmin,
-                       float tmax_entry, float closest, bool prune, float delta) {
+                       float tmax_entry, float closest, bool prune, float dmi) {
     float te;
     bool go = slab(x0, y0, z0, x1, y1, z1, r, inv, tmin, tmax_entry, te);
-    if (go && prune) {
-        te = slab_entry_inflated(x0, y0, z0, x1, y1, z1, r, inv, tmin, delta);
-        go = !(te > prune_bound(closest));
-    }
+    if (prune) te = te - dmi;
+    if (go && prune) go = !(te > prune_bound(closest));
     return go ? (te < 3.4028235e38f ? te : 3.4028235e38f) : kInf;  // visited children sort first
 }
 RT_DEV void sort2(float& ta, uint32_t& ca, float& tb, uint32_t& cb) {
@@ -822,6 +817,7 @@ RT_DEV bool bvh_hit(const DevScene& S, float delta, uint32_t root, const Ray& r,
         return false;
     }
     const bool prune = (__float_as_uint(wrapper[7].w) & rtdev::kBvhPrunable) != 0u;
+    const float dmi = delta * fmaxf(fmaxf(__builtin_fabsf(inv.x), __builtin_fabsf(inv.y)), __builtin_fabsf(inv.z));
     const bool leaf_boxes = prune && !(mode & kModeNoLeafBoxes);
     bool any = false;
     uint32_t best_rank = 0, sp = 0, cur = root;
@@ -907,46 +903,23 @@ RT_DEV bool bvh_hit(const DevScene& S, float delta, uint32_t root, const Ray& r,
             c1 = __float_as_uint(chf.y);
             c2 = __float_as_uint(chf.z);
             c3 = __float_as_uint(chf.w);
-            // The inflated-entry pass can only prune once closest is finite
-            // (prune_bound(inf) = inf); while no active lane has a hit yet, the
-            // whole wave skips it.
-            const bool prune_now = prune && closest < kInf;
             ABLATE(kAbKeys2, float k2 = child_key(mnx.x, mny.x, mnz.x, mxx.x, mxy.x, mxz.x, r, inv, tmin, tmax_entry,
-                                                  closest, prune_now, delta) +
+                                                  closest, prune, dmi) +
                                         child_key(mnx.y, mny.y, mnz.y, mxx.y, mxy.y, mxz.y, r, inv, tmin, tmax_entry,
-                                                  closest, prune_now, delta) +
+                                                  closest, prune, dmi) +
                                         child_key(mnx.z, mny.z, mnz.z, mxx.z, mxy.z, mxz.z, r, inv, tmin, tmax_entry,
-                                                  closest, prune_now, delta) +
+                                                  closest, prune, dmi) +
                                         child_key(mnx.w, mny.w, mnz.w, mxx.w, mxy.w, mxz.w, r, inv, tmin, tmax_entry,
-                                                  closest, prune_now, delta);
+                                                  closest, prune, dmi);
                    if (k2 == -1.0f) c0 = 0u;);
-            if (__ballot(prune_now) != 0ull) {
-                if (c0 != rtdev::kChildEmpty)
-                    t0 = child_key(mnx.x, mny.x, mnz.x, mxx.x, mxy.x, mxz.x, r, inv, tmin, tmax_entry, closest,
-                                   prune_now, delta);
-                if (c1 != rtdev::kChildEmpty)
-                    t1 = child_key(mnx.y, mny.y, mnz.y, mxx.y, mxy.y, mxz.y, r, inv, tmin, tmax_entry, closest,
-                                   prune_now, delta);
-                if (c2 != rtdev::kChildEmpty)
-                    t2 = child_key(mnx.z, mny.z, mnz.z, mxx.z, mxy.z, mxz.z, r, inv, tmin, tmax_entry, closest,
-                                   prune_now, delta);
-                if (c3 != rtdev::kChildEmpty)
-                    t3 = child_key(mnx.w, mny.w, mnz.w, mxx.w, mxy.w, mxz.w, r, inv, tmin, tmax_entry, closest,
-                                   prune_now, delta);
-            } else {
-                if (c0 != rtdev::kChildEmpty)
-                    t0 = child_key(mnx.x, mny.x, mnz.x, mxx.x, mxy.x, mxz.x, r, inv, tmin, tmax_entry, closest, false,
-                                   delta);
-                if (c1 != rtdev::kChildEmpty)
-                    t1 = child_key(mnx.y, mny.y, mnz.y, mxx.y, mxy.y, mxz.y, r, inv, tmin, tmax_entry, closest, false,
-                                   delta);
-                if (c2 != rtdev::kChildEmpty)
-                    t2 = child_key(mnx.z, mny.z, mnz.z, mxx.z, mxy.z, mxz.z, r, inv, tmin, tmax_entry, closest, false,
-                                   delta);
-                if (c3 != rtdev::kChildEmpty)
-                    t3 = child_key(mnx.w, mny.w, mnz.w, mxx.w, mxy.w, mxz.w, r, inv, tmin, tmax_entry, closest, false,
-                                   delta);
-            }
+            if (c0 != rtdev::kChildEmpty)
+                t0 = child_key(mnx.x, mny.x, mnz.x, mxx.x, mxy.x, mxz.x, r, inv, tmin, tmax_entry, closest, prune, dmi);
+            if (c1 != rtdev::kChildEmpty)
+                t1 = child_key(mnx.y, mny.y, mnz.y, mxx.y, mxy.y, mxz.y, r, inv, tmin, tmax_entry, closest, prune, dmi);
+            if (c2 != rtdev::kChildEmpty)
+                t2 = child_key(mnx.z, mny.z, mnz.z, mxx.z, mxy.z, mxz.z, r, inv, tmin, tmax_entry, closest, prune, dmi);
+            if (c3 != rtdev::kChildEmpty)
+                t3 = child_key(mnx.w, mny.w, mnz.w, mxx.w, mxy.w, mxz.w, r, inv, tmin, tmax_entry, closest, prune, dmi);
         }
         PROF_ADD(kPrBvhTrip, pt);
         PROF_T0(pp);
@@ -1936,6 +1909,14 @@ int rt_scene_upload(const rt_scene_desc* desc, int device, rt_scene_handle* out)
     d.num_top = hs.num_top;
     d.num_entries = (uint32_t)hs.entries.size();
     d.stack_depth = hs.max_stack;
+#ifdef RT_LEAF_AUDIT
+    // the audit replays every fast traversal with the BVH2 recursion on the same stack
+    d.stack_depth = std::max(hs.max_stack, hs.max_stack_ref);
+#endif
+#ifdef RT_LEAF_AUDIT
+    // the audit replays every fast traversal with the BVH2 recursion on the same stack
+    d.stack_depth = std::max(hs.max_stack, hs.max_stack_ref);
+#endif
     s->stack_ref = hs.max_stack_ref;
     d.perm_bytes = (uint32_t)hs.perm.size();
     d.hrpp_tab = nullptr;  // set per RT_FLAG_HRPP launch

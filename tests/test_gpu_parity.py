@@ -232,3 +232,22 @@ def test_pruned_traversal_equals_reference_traversal_full_frame(cfg_name, spp, r
     ds.close()
     np.testing.assert_array_equal(out[True][0], out[False][0])
     assert out[True][1]["segments"] == out[False][1]["segments"]
+
+
+def test_traversal_audit_full_c3_frame():
+    # The audit build replays EVERY fast BVH traversal of a full C3 frame (500 spp)
+    # with the literal bvh.rs recursion and re-tests every leaf-box reject; both
+    # counts must be 0. Per-call (t, primitive) equality is stricter than the image
+    # tests: a tie resolved to the wrong coplanar face can shade identically.
+    import subprocess
+    import sys
+    root = os.path.dirname(HERE)
+    lib = os.path.join(root, "raytracinginoneweekendinrust_amd", "_lib", "librtamd_audit.so")
+    assert os.path.exists(lib), "build() makes the audit library"
+    env = dict(os.environ, RT_LIBRARY=lib)
+    r = subprocess.run([sys.executable, os.path.join(root, "tools", "region_profile.py"), "--config", "C3",
+                        "--spp", "500"], capture_output=True, text=True, env=env, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = r.stdout + r.stderr
+    assert '{"leaf_audit_count": 0}' in out, out[-2000:]
+    assert '{"trav_audit_count": 0}' in out, out[-2000:]
