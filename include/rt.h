@@ -123,6 +123,13 @@ typedef struct rt_camera_desc {
                                  empty at each launch and are filled concurrently,
                                  so results are NOT deterministic (neither are
                                  the reference's, bvh.rs:146-149)             */
+/* Progressive (time-sliced) rendering: a frame of S spp rendered as slices
+ * [b, e) — sample_base = b, samples_per_pixel = e - b, spp_total = S — gives the
+ * one-shot image bit for bit, because every pixel's sum keeps sample order: */
+#define RT_FLAG_ACCUMULATE 4u /* the slice continues the running sum already in
+                                 the output instead of starting from zero      */
+#define RT_FLAG_RAW_SUM 8u    /* leave the running sum in the output (no final
+                                 division): every slice but the last           */
 
 typedef struct rt_render_params {
     uint32_t width, height;      /* image size (Renderer::from_aspect_ratio)        */
@@ -135,7 +142,8 @@ typedef struct rt_render_params {
     uint32_t shard_count;        /*   b % shard_count == shard_index (0/1 = all)    */
     uint32_t flags;              /* RT_FLAG_*                                       */
     float background[3];         /* src/main.rs:155-164                             */
-    uint32_t reserved1;
+    uint32_t spp_total;          /* divisor of the final average; 0 = samples_per_pixel
+                                    (set to the frame's spp for the last slice)    */
 } rt_render_params;
 
 typedef struct rt_stats {

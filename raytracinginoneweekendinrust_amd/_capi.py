@@ -22,6 +22,8 @@ RT_MAT_LAMBERTIAN, RT_MAT_METAL, RT_MAT_DIELECTRIC, RT_MAT_DIFFUSE_LIGHT, RT_MAT
 
 RT_FLAG_EXACT_BVH = 1
 RT_FLAG_HRPP = 2
+RT_FLAG_ACCUMULATE = 4
+RT_FLAG_RAW_SUM = 8
 
 STATUS = {0: "RT_OK", -1: "RT_ERR_INVALID", -2: "RT_ERR_UNSUPPORTED", -3: "RT_ERR_HIP", -4: "RT_ERR_OOM",
           -5: "RT_ERR_NO_DEVICE", -6: "RT_ERR_IO"}
@@ -48,7 +50,7 @@ class rt_render_params(C.Structure):
                 ("max_depth", C.c_uint32), ("tile_width", C.c_uint32), ("tile_height", C.c_uint32),
                 ("seed", C.c_uint64), ("sample_base", C.c_uint32), ("shard_index", C.c_uint32),
                 ("shard_count", C.c_uint32), ("flags", C.c_uint32), ("background", C.c_float * 3),
-                ("reserved1", C.c_uint32)]
+                ("spp_total", C.c_uint32)]
 
 
 class rt_stats(C.Structure):

@@ -161,6 +161,7 @@ struct DevParams {
     float bg[3];
     float prune_delta;  // box inflation for closest-hit pruning ("exact pruning")
     uint32_t tune;      // kMode* traversal switches from RT_TUNE (diagnostics)
+    uint32_t spp_div;   // divisor of the final average (rt_render_params.spp_total or spp)
 };
 
 }  // namespace rtdev

@@ -1685,7 +1685,7 @@ __global__ __launch_bounds__(256) void resolve_samples(const float* __restrict__
         acc = acc + mk(src[0], src[1], src[2]);
         src += plane;
     }
-    if (last) acc = divs(acc, (float)P.spp);
+    if (last) acc = divs(acc, (float)P.spp_div);
     o[0] = acc.x;
     o[1] = acc.y;
     o[2] = acc.z;
@@ -2065,6 +2065,7 @@ int rt_render_launch(rt_scene_handle s, const rt_camera_desc* camera, const rt_r
     dp.blocks_x = (p->width + 7u) / 8u;
     dp.num_blocks = dp.blocks_x * ((p->height + 7u) / 8u);
     dp.flags = p->flags;
+    dp.spp_div = p->spp_total ? p->spp_total : p->samples_per_pixel;
     {
         const char* tune = getenv("RT_TUNE");  // diagnostic traversal switches (kMode* bits), default 0
         dp.tune = tune ? (uint32_t)strtoul(tune, nullptr, 0) & ~kModeExact : 0u;
@@ -2199,7 +2200,8 @@ int rt_render_launch(rt_scene_handle s, const rt_camera_desc* camera, const rt_r
             s->ev_count++;
         }
         hipLaunchKernelGGL(resolve_samples, dim3((uint32_t)((npix + 255u) / 256u)), dim3(256), 0, st, s->sbuf, d_out, dp,
-                           q, c == 0 ? 1 : 0, c + 1 == nchunks ? 1 : 0);
+                           q, c == 0 && !(p->flags & RT_FLAG_ACCUMULATE) ? 1 : 0,
+                           c + 1 == nchunks && !(p->flags & RT_FLAG_RAW_SUM) ? 1 : 0);
         if ((e = hipGetLastError()) != hipSuccess) return hip_fail(e, "resolve_samples launch");
     }
     return RT_OK;

@@ -107,3 +107,18 @@ def test_shimmer_cli_writes_the_reference_ppm(rt, tmp_path):
     want, _ = ds.render(cfg.camera(), params)
     ds.close()
     np.testing.assert_array_equal(img, want)
+
+
+@pytest.mark.parametrize("slices", [[16], [8, 8], [3, 5, 8], [1] * 16])
+def test_progressive_slices_equal_the_one_shot_render(slices, rt):
+    # RT_FLAG_ACCUMULATE / RT_FLAG_RAW_SUM keep every pixel's sum in sample order,
+    # so the last slice's image is the one-shot frame bit for bit
+    cfg, scene, params = c3(rt, 64, 16)
+    ds = rt.DeviceScene(scene)
+    want, _ = ds.render(cfg.camera(), params)
+    done, img = 0, None
+    for done, img in rt.render_progressive(ds, cfg.camera(), params, slices):
+        assert np.isfinite(img).all()
+    ds.close()
+    assert done == 16
+    np.testing.assert_array_equal(img, want)
