@@ -55,6 +55,8 @@ enum EntryKind : uint32_t {
     kEntGeom = 0,    // payload = leaf code of one primitive / cube
     kEntBvh = 1,     // payload = root node index
     kEntMedium = 2,  // payload = boundary entry index; phase_mat, neg_inv_density
+    kEntSphereRun = 3,  // payload = first sphere, pad[0] = count: consecutive top-level spheres
+                        // (no transforms, consecutive sphere records), tested in list order
 };
 
 constexpr int kMaxTransforms = 3;

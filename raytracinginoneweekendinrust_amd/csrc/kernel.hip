@@ -1022,6 +1022,20 @@ RT_DEV bool entry_geom_hit(const DevScene& S, float delta, const DevEntry* E, Ra
                            uint32_t& hit_code, uint32_t* stk, uint32_t mode, bool& replay) {
     uint32_t ntf = E->ntf;
     for (uint32_t i = 0; i < ntf; ++i) r = apply_op(E->tf[i], r);
+    if (E->kind == rtdev::kEntSphereRun) {  // consecutive top-level spheres, in list order
+        const uint32_t first = E->payload, n = E->pad[0];
+        const RayD q = to_d(r);
+        bool any = false;
+        for (uint32_t i = 0; i < n; ++i) {
+            float t;
+            if (sphere_t(ld4(S.sph + first + i), q, tmin, closest, t)) {
+                closest = t;
+                hit_code = rtdev::leaf_code(rtdev::kLeafSphere, first + i);
+                any = true;
+            }
+        }
+        return any;
+    }
     if (E->kind == rtdev::kEntBvh) {
         ABLATE(kAbBvh2, float c2 = closest; uint32_t h2 = 0u; bool rp = false;
                if (bvh_hit<kKind>(S, delta, E->payload, r, tmin, c2, h2, stk, mode, rp) && h2 == 0x7fffffffu)

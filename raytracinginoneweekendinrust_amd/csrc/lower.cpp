@@ -220,6 +220,31 @@ class Lowerer {
         Chain chain;
         int rc = lower_entry(d_->world, chain, &top, 0);
         if (rc) return rc;
+        // Consecutive untransformed spheres with consecutive records become one
+        // run entry (hittable.rs:100-118 order and closest_so_far unchanged): the
+        // device then streams the sphere records without per-entry headers.
+        std::vector<rtdev::DevEntry> merged;
+        for (const auto& e : top) {
+            const bool sph = e.kind == rtdev::kEntGeom && e.ntf == 0 &&
+                             rtdev::leaf_type(e.payload) == rtdev::kLeafSphere;
+            if (sph && !merged.empty()) {
+                rtdev::DevEntry& b = merged.back();
+                const bool bsph = b.kind == rtdev::kEntGeom && b.ntf == 0 &&
+                                  rtdev::leaf_type(b.payload) == rtdev::kLeafSphere;
+                const uint32_t bfirst = rtdev::leaf_index(b.payload), bn = b.kind == rtdev::kEntSphereRun ? b.pad[0] : 1u;
+                if ((b.kind == rtdev::kEntSphereRun || bsph) && (b.kind == rtdev::kEntSphereRun ? b.payload : bfirst) + bn ==
+                                                                   rtdev::leaf_index(e.payload)) {
+                    if (b.kind != rtdev::kEntSphereRun) {
+                        b.kind = rtdev::kEntSphereRun;
+                        b.payload = bfirst;
+                    }
+                    b.pad[0] = bn + 1u;
+                    continue;
+                }
+            }
+            merged.push_back(e);
+        }
+        top.swap(merged);
         s_->num_top = (uint32_t)top.size();
         for (auto& e : top)
             if (e.kind == rtdev::kEntMedium) e.payload += s_->num_top;
