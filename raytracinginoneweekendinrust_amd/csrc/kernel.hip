@@ -783,11 +783,48 @@ RT_DEV float child_key(float x0, float y0, float z0, float x1, float y1, float z
     if (go && prune) go = !(te > prune_bound(closest));
     return go ? (te < 3.4028235e38f ? te : 3.4028235e38f) : kInf;  // visited children sort first
 }
-RT_DEV void sort2(float& ta, uint32_t& ca, float& tb, uint32_t& cb) {
-    if (tb < ta) {
-        float t = ta; ta = tb; tb = t;
-        uint32_t c = ca; ca = cb; cb = c;
+// child_key for all four slots of a node at once, on two children per packed
+// f32 instruction (v_pk_add_f32 / v_pk_mul_f32: the same correctly rounded IEEE
+// operations per element). Valid only without NaN slab values: the fast kernel
+// replays every ray with a zero or non-finite 1/d component, so (plane - o) * inv
+// is finite or +-inf, never 0 * inf, and the reference's sequential
+// `if a > t_min {a} else {t_min}` clamps (aabb.rs:28-41) equal max/min. Empty
+// slots hold an inverted infinite box (lower.cpp) and never pass. dmi = 0 and
+// pb = +inf when the BVH is not prunable.
+typedef float pk2 __attribute__((ext_vector_type(2)));
+RT_DEV pk2 pk(float a, float b) { return pk2{a, b}; }
+RT_DEV void child_keys4(f4 mnx, f4 mny, f4 mnz, f4 mxx, f4 mxy, f4 mxz, const Ray& r, V inv, float tmin,
+                        float tmax_entry, float pb, float dmi, float key[4]) {
+    const pk2 ox = pk(r.o.x, r.o.x), oy = pk(r.o.y, r.o.y), oz = pk(r.o.z, r.o.z);
+    const pk2 ix = pk(inv.x, inv.x), iy = pk(inv.y, inv.y), iz = pk(inv.z, inv.z);
+    const bool sx = inv.x < 0.0f, sy = inv.y < 0.0f, sz = inv.z < 0.0f;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const pk2 ax = (h ? pk(mnx.z, mnx.w) : pk(mnx.x, mnx.y)) - ox, bx = (h ? pk(mxx.z, mxx.w) : pk(mxx.x, mxx.y)) - ox;
+        const pk2 ay = (h ? pk(mny.z, mny.w) : pk(mny.x, mny.y)) - oy, by = (h ? pk(mxy.z, mxy.w) : pk(mxy.x, mxy.y)) - oy;
+        const pk2 az = (h ? pk(mnz.z, mnz.w) : pk(mnz.x, mnz.y)) - oz, bz = (h ? pk(mxz.z, mxz.w) : pk(mxz.x, mxz.y)) - oz;
+        const pk2 tax = ax * ix, tbx = bx * ix, tay = ay * iy, tby = by * iy, taz = az * iz, tbz = bz * iz;
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const float nx = sx ? tbx[e] : tax[e], fx = sx ? tax[e] : tbx[e];
+            const float ny = sy ? tby[e] : tay[e], fy = sy ? tay[e] : tby[e];
+            const float nz = sz ? tbz[e] : taz[e], fz = sz ? taz[e] : tbz[e];
+            const float lo = __builtin_fmaxf(__builtin_fmaxf(nx, ny), __builtin_fmaxf(nz, tmin));
+            const float hi = __builtin_fminf(__builtin_fminf(fx, fy), __builtin_fminf(fz, tmax_entry));
+            const float te = lo - dmi;
+            const bool go = lo <= hi && te <= pb;  // = !(hi < lo) && !(te > pb) without NaN
+            key[2 * h + e] = go ? __builtin_fminf(te, 3.4028235e38f) : kInf;
+        }
     }
+}
+RT_DEV void sort2(float& ta, uint32_t& ca, float& tb, uint32_t& cb) {  // branch-free compare-exchange
+    const bool sw = tb < ta;
+    const float a = ta, b = tb;
+    const uint32_t x = ca, y = cb;
+    ta = sw ? b : a;
+    tb = sw ? a : b;
+    ca = sw ? y : x;
+    cb = sw ? x : y;
 }
 // kKind 0: the fast BVH4 kernel; 1: the reference kernel replays bvh.rs literally;
 // 2: the reference kernel with HRPP predictors (RT_FLAG_HRPP experiment). The fast kernel
@@ -812,9 +849,17 @@ RT_DEV bool bvh_hit(const DevScene& S, float delta, uint32_t root, const Ray& r,
         }
         return bvh_hit_reference(S, w2, r, q, inv, tmin, closest, hit_code, stk);
     }
-    if (r.d.x == 0.0f || r.d.y == 0.0f || r.d.z == 0.0f) {
-        replay = true;
-        return false;
+    // Only rays with 0 < |1/d| < inf on every axis stay here: a zero component
+    // (1/d = inf: NaN rect hits), a denormal one (1/d = inf) or a non-finite one
+    // (1/d = 0 or NaN, e.g. H = 1 images divide by H - 1 = 0 in renderer.rs:141)
+    // would give 0 * inf = NaN slab values, which the packed child test and the
+    // empty slots' infinite boxes must never see. The reference kernel takes them.
+    {
+        const float ax = __builtin_fabsf(inv.x), ay = __builtin_fabsf(inv.y), az = __builtin_fabsf(inv.z);
+        if (!(ax > 0.0f && ax < kInf && ay > 0.0f && ay < kInf && az > 0.0f && az < kInf)) {
+            replay = true;
+            return false;
+        }
     }
     const bool prune = (__float_as_uint(wrapper[7].w) & rtdev::kBvhPrunable) != 0u;
     const float dmi = delta * fmaxf(fmaxf(__builtin_fabsf(inv.x), __builtin_fabsf(inv.y)), __builtin_fabsf(inv.z));
@@ -912,14 +957,13 @@ RT_DEV bool bvh_hit(const DevScene& S, float delta, uint32_t root, const Ray& r,
                                         child_key(mnx.w, mny.w, mnz.w, mxx.w, mxy.w, mxz.w, r, inv, tmin, tmax_entry,
                                                   closest, prune, dmi);
                    if (k2 == -1.0f) c0 = 0u;);
-            if (c0 != rtdev::kChildEmpty)
-                t0 = child_key(mnx.x, mny.x, mnz.x, mxx.x, mxy.x, mxz.x, r, inv, tmin, tmax_entry, closest, prune, dmi);
-            if (c1 != rtdev::kChildEmpty)
-                t1 = child_key(mnx.y, mny.y, mnz.y, mxx.y, mxy.y, mxz.y, r, inv, tmin, tmax_entry, closest, prune, dmi);
-            if (c2 != rtdev::kChildEmpty)
-                t2 = child_key(mnx.z, mny.z, mnz.z, mxx.z, mxy.z, mxz.z, r, inv, tmin, tmax_entry, closest, prune, dmi);
-            if (c3 != rtdev::kChildEmpty)
-                t3 = child_key(mnx.w, mny.w, mnz.w, mxx.w, mxy.w, mxz.w, r, inv, tmin, tmax_entry, closest, prune, dmi);
+            float key[4];
+            child_keys4(mnx, mny, mnz, mxx, mxy, mxz, r, inv, tmin, tmax_entry, prune ? prune_bound(closest) : kInf,
+                        prune ? dmi : 0.0f, key);
+            t0 = key[0];
+            t1 = key[1];
+            t2 = key[2];
+            t3 = key[3];
         }
         PROF_ADD(kPrBvhTrip, pt);
         PROF_T0(pp);
@@ -2209,6 +2253,12 @@ int rt_render_launch(rt_scene_handle s, const rt_camera_desc* camera, const rt_r
                                s->sbuf, s->counter, s->replay, 1u, d_segments);
         }
         if ((e = hipGetLastError()) != hipSuccess) return hip_fail(e, "trace_samples launch");
+        if (getenv("RT_REPLAY_LOG")) {  // diagnostics: samples the fast kernel handed to the reference kernel
+            TraceCounters h{};
+            if (hipMemcpyAsync(&h, s->counter, sizeof h, hipMemcpyDeviceToHost, st) == hipSuccess &&
+                hipStreamSynchronize(st) == hipSuccess)
+                fprintf(stderr, "rt: chunk %u: %u samples replayed by the reference kernel\n", c, h.replay_count);
+        }
         if (evp) {
             (void)hipEventRecord(evp[1], st);
             s->ev_count++;

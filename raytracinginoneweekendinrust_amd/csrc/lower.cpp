@@ -720,7 +720,9 @@ class Lowerer {
             uint32_t ch[4], rk[4];
             for (uint32_t k = 0; k < 4; ++k) {
                 const bool have = k < sl.size();
-                const Box b = have ? sl[k].box : Box{{0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f}};
+                // an empty slot holds an inverted infinite box: its slab interval is
+                // empty for every finite ray (the device's child_keys4 needs no check)
+                const Box b = have ? sl[k].box : Box{{INFINITY, INFINITY, INFINITY}, {-INFINITY, -INFINITY, -INFINITY}};
                 mnx[k] = b.mn.x; mny[k] = b.mn.y; mnz[k] = b.mn.z;
                 mxx[k] = b.mx.x; mxy[k] = b.mx.y; mxz[k] = b.mx.z;
                 if (!have) {
