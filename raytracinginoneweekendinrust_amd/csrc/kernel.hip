@@ -63,7 +63,7 @@ enum ProfRegion : uint32_t {
 };
 // traversal mode bits (bvh_hit): kModeExact = RT_FLAG_EXACT_BVH; the rest come
 // from DevParams::tune (RT_TUNE environment variable, diagnostics / A-B runs).
-constexpr uint32_t kModeExact = 1u, kModeNoLeafBoxes = 2u;
+constexpr uint32_t kModeExact = 1u, kModeNoLeafBoxes = 2u, kModeNoPermLds = 32u, kModeW3 = 64u;
 #ifdef RT_ABLATE
 // Ablation build (librtamd_ablate.so, diagnostics only): RT_TUNE bits that run a
 // piece of work twice (results of the copy discarded through an opaque test),
@@ -817,6 +817,36 @@ RT_DEV void child_keys4(f4 mnx, f4 mny, f4 mnz, f4 mxx, f4 mxy, f4 mxz, const Ra
         }
     }
 }
+// The two leaf slots of a leaf node: the slab interval of each leaf's box
+// inflated by delta (leaf_box_may_hit's lo / hi), both leaves per packed
+// instruction. The inflation is folded into shifted origins: x0 - (o + delta)
+// carries the same error structure as (x0 - delta) - o (one rounding of a
+// coordinate-sized value, <= 2^-24 R << delta, then relative roundings). NaN-free
+// under the same 1/d condition as child_keys4; an empty second slot (inverted
+// infinite box) gives lo = +inf.
+RT_DEV void leaf_intervals2(float2 bx0, float2 by0, float2 bz0, float2 bx1, float2 by1, float2 bz1, const Ray& r,
+                            V inv, float delta, float lo[2], float hi[2]) {
+    const pk2 px = pk(r.o.x + delta, r.o.x + delta), py = pk(r.o.y + delta, r.o.y + delta),
+              pz = pk(r.o.z + delta, r.o.z + delta);
+    const pk2 mx = pk(r.o.x - delta, r.o.x - delta), my = pk(r.o.y - delta, r.o.y - delta),
+              mz = pk(r.o.z - delta, r.o.z - delta);
+    const pk2 ix = pk(inv.x, inv.x), iy = pk(inv.y, inv.y), iz = pk(inv.z, inv.z);
+    const pk2 tax = (pk(bx0.x, bx0.y) - px) * ix, tbx = (pk(bx1.x, bx1.y) - mx) * ix;
+    const pk2 tay = (pk(by0.x, by0.y) - py) * iy, tby = (pk(by1.x, by1.y) - my) * iy;
+    const pk2 taz = (pk(bz0.x, bz0.y) - pz) * iz, tbz = (pk(bz1.x, bz1.y) - mz) * iz;
+    const bool sx = inv.x < 0.0f, sy = inv.y < 0.0f, sz = inv.z < 0.0f;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+        lo[e] = __builtin_fmaxf(__builtin_fmaxf(sx ? tbx[e] : tax[e], sy ? tby[e] : tay[e]), sz ? tbz[e] : taz[e]);
+        hi[e] = __builtin_fminf(__builtin_fminf(sx ? tax[e] : tbx[e], sy ? tay[e] : tby[e]), sz ? taz[e] : tbz[e]);
+    }
+}
+// leaf_box_may_hit's decision on a precomputed inflated interval.
+RT_DEV bool leaf_interval_may_hit(float lo, float hi, float tmin, float closest) {
+    if (lo > prune_bound(closest)) return false;
+    if (tmin > 0.0f && hi < tmin * (1.0f - 0x1p-19f)) return false;
+    return !(lo - hi > (__builtin_fabsf(lo) + __builtin_fabsf(hi)) * 0x1p-19f);
+}
 RT_DEV void sort2(float& ta, uint32_t& ca, float& tb, uint32_t& cb) {  // branch-free compare-exchange
     const bool sw = tb < ta;
     const float a = ta, b = tb;
@@ -895,13 +925,15 @@ RT_DEV bool bvh_hit(const DevScene& S, float delta, uint32_t root, const Ray& r,
             bool nh = false;
             uint32_t ncode = 0u, nrank = 0u;
             const uint32_t nleaf = __float_as_uint(chs.y) == rtdev::kChildEmpty ? 1u : 2u;
+            float llo[2] = {-kInf, -kInf}, lhi[2] = {kInf, kInf};
+            if (leaf_boxes) leaf_intervals2(bx0, by0, bz0, bx1, by1, bz1, r, inv, delta, llo, lhi);
             for (uint32_t k = 0; k < nleaf; ++k) {
                 const uint32_t lcode = __float_as_uint(k ? chs.y : chs.x), rank = __float_as_uint(k ? rks.y : rks.x);
                 const float x0 = k ? bx0.y : bx0.x, y0 = k ? by0.y : by0.x, z0 = k ? bz0.y : bz0.x;
                 const float x1 = k ? bx1.y : bx1.x, y1 = k ? by1.y : by1.x, z1 = k ? bz1.y : bz1.x;
                 // the right leaf can only matter if t <= min(closest, left t)
                 const float bound = tmr < closest ? tmr : closest;
-                if (!leaf_boxes || leaf_box_may_hit(x0, y0, z0, x1, y1, z1, r, inv, tmin, bound, delta)) {
+                if (!leaf_boxes || leaf_interval_may_hit(k ? llo[1] : llo[0], k ? lhi[1] : lhi[0], tmin, bound)) {
                     PROF_T0(pl);
                     // Only candidates whose f32 t can tie or beat closest matter, so
                     // the test may use min(t_max, nextup(closest)): a root in
@@ -1629,11 +1661,11 @@ RT_DEV bool finish_segment(const DevScene& S, const DevParams& P, const ChunkPar
 // fixup kernel re-renders the whole chunk and takes back the fast kernel's
 // segment count.
 constexpr uint32_t kReplayCap = 1u << 20;
-template <int kKind>
-#ifndef RT_TRACE_MIN_WAVES
-#define RT_TRACE_MIN_WAVES 1  // waves/SIMD the register allocator must allow (build-time tuning)
-#endif
-__global__ __launch_bounds__(64, RT_TRACE_MIN_WAVES) void trace_samples(DevScene Sg, DevCamera C, DevParams P, ChunkParams Q,
+// kWaves: the waves per SIMD the register allocator must allow. 3 (<= 168 VGPRs)
+// is the default; the fast kernel also exists at 4 (<= 128 VGPRs, a few spills),
+// launched when the scene's LDS stack fits four waves per SIMD (rt_render_launch).
+template <int kKind, int kWaves = 3>
+__global__ __launch_bounds__(64, kWaves) void trace_samples(DevScene Sg, DevCamera C, DevParams P, ChunkParams Q,
                                                     float* __restrict__ sbuf, TraceCounters* __restrict__ ctr,
                                                     ReplayItem* __restrict__ replay_list, uint32_t fixup,
                                                     unsigned long long* __restrict__ seg_counter) {
@@ -1643,7 +1675,7 @@ __global__ __launch_bounds__(64, RT_TRACE_MIN_WAVES) void trace_samples(DevScene
     // Perlin permutation tables (Marble) behind the stack when they fit: the
     // three dependent byte lookups per lattice corner then hit LDS, not L2.
     DevScene S = Sg;
-    if (S.perm_bytes != 0u && S.perm_bytes <= kPermLdsMax) {
+    if (S.perm_bytes != 0u && S.perm_bytes <= kPermLdsMax && !(P.tune & kModeNoPermLds)) {
         uint32_t* tab = lds_stack + S.stack_depth * 128u;
         const uint32_t* src = reinterpret_cast<const uint32_t*>(Sg.perm);
         for (uint32_t i = lane; i < S.perm_bytes / 4u; i += 64u) tab[i] = src[i];
@@ -1651,7 +1683,8 @@ __global__ __launch_bounds__(64, RT_TRACE_MIN_WAVES) void trace_samples(DevScene
         S.perm = reinterpret_cast<const uint8_t*>(tab);
     }
     if (kKind == 2) {  // HRPP counters behind the stack and the Perlin tables
-        const uint32_t perm_words = S.perm_bytes != 0u && S.perm_bytes <= kPermLdsMax ? S.perm_bytes / 4u : 0u;
+        const uint32_t perm_words =
+            S.perm_bytes != 0u && S.perm_bytes <= kPermLdsMax && !(P.tune & kModeNoPermLds) ? S.perm_bytes / 4u : 0u;
         S.hrpp_cnt = lds_stack + S.stack_depth * 128u + perm_words;
         if (lane < 4u * S.hrpp_npred) S.hrpp_cnt[lane] = 0u;
         __syncthreads();
@@ -1813,6 +1846,7 @@ struct rt_scene {
     TraceCounters* counter = nullptr;
     uint32_t stack_ref = 1;  // LDS stack entries per lane of trace_samples<1, 2> (dev.stack_depth: <0>)
     int grid = 0, grid_ref = 0;  // resident waves of trace_samples<0> / <1>
+    int fast_waves = 0;          // 3 or 4: the trace_samples<0, kWaves> instance this scene launches
     ReplayItem* replay = nullptr;  // kReplayCap entries
     float coord_bound = 0.0f;
     // HRPP experiment: tables (allocated at the first RT_FLAG_HRPP render) and counters
@@ -1967,10 +2001,6 @@ int rt_scene_upload(const rt_scene_desc* desc, int device, rt_scene_handle* out)
     d.num_top = hs.num_top;
     d.num_entries = (uint32_t)hs.entries.size();
     d.stack_depth = hs.max_stack;
-#ifdef RT_LEAF_AUDIT
-    // the audit replays every fast traversal with the BVH2 recursion on the same stack
-    d.stack_depth = std::max(hs.max_stack, hs.max_stack_ref);
-#endif
 #ifdef RT_LEAF_AUDIT
     // the audit replays every fast traversal with the BVH2 recursion on the same stack
     d.stack_depth = std::max(hs.max_stack, hs.max_stack_ref);
@@ -2172,10 +2202,24 @@ int rt_render_launch(rt_scene_handle s, const rt_camera_desc* camera, const rt_r
         if ((e = hipMalloc(&s->replay, sizeof(ReplayItem) * (size_t)kReplayCap)) != hipSuccess)
             return rthost::set_error(RT_ERR_OOM, std::string("hipMalloc replay list: ") + hipGetErrorString(e));
     }
+    // The fast kernel's instance: four waves per SIMD when that raises its occupancy
+    // over three (the Perlin tables then stay in L2, so the stack alone sets LDS).
+    if (s->fast_waves == 0) {
+        const size_t stack_lds = (size_t)s->dev.stack_depth * 128u * sizeof(uint32_t);
+        const size_t perm3 = s->dev.perm_bytes != 0u && s->dev.perm_bytes <= kPermLdsMax ? s->dev.perm_bytes : 0u;
+        int per3 = 0, per4 = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per3, trace_samples<0, 3>, 64, stack_lds + perm3) != hipSuccess)
+            per3 = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per4, trace_samples<0, 4>, 64, stack_lds) != hipSuccess)
+            per4 = 0;
+        s->fast_waves = per4 > per3 && !(dp.tune & kModeW3) ? 4 : 3;
+    }
+    if (s->fast_waves == 4) dp.tune |= kModeNoPermLds;
     // LDS per wave: the kernel's traversal stack, then the Perlin tables
     DevScene dev_ref = s->dev;
     dev_ref.stack_depth = s->stack_ref;
-    const size_t perm_lds = s->dev.perm_bytes != 0u && s->dev.perm_bytes <= kPermLdsMax ? s->dev.perm_bytes : 0u;
+    const size_t perm_lds =
+        s->dev.perm_bytes != 0u && s->dev.perm_bytes <= kPermLdsMax && !(dp.tune & kModeNoPermLds) ? s->dev.perm_bytes : 0u;
     const size_t lds = (size_t)s->dev.stack_depth * 128u * sizeof(uint32_t) + perm_lds;
     size_t lds_ref = (size_t)dev_ref.stack_depth * 128u * sizeof(uint32_t) + perm_lds;
     if ((dp.flags & RT_FLAG_HRPP) && s->dev.hrpp_npred) {  // the experiment: reference kernel + predictors
@@ -2205,7 +2249,9 @@ int rt_render_launch(rt_scene_handle s, const rt_camera_desc* camera, const rt_r
     }
     if (s->grid == 0) {
         int per_cu = 0, per_cu_ref = 0, cus = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace_samples<0>, 64, lds) != hipSuccess ||
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, s->fast_waves == 4 ? trace_samples<0, 4>
+                                                                                      : trace_samples<0, 3>,
+                                                         64, lds) != hipSuccess ||
             per_cu < 1)
             per_cu = 8;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_ref, trace_samples<1>, 64, lds_ref) != hipSuccess ||
@@ -2215,6 +2261,9 @@ int rt_render_launch(rt_scene_handle s, const rt_camera_desc* camera, const rt_r
             cus = 256;
         s->grid = per_cu * cus;
         s->grid_ref = per_cu_ref * cus;
+        if (getenv("RT_REPLAY_LOG"))
+            fprintf(stderr, "rt: trace_samples<0, %d>: %d waves/CU (LDS %zu B/wave), reference kernel %d waves/CU\n",
+                    s->fast_waves, per_cu, lds, per_cu_ref);
     }
     const bool exact = (dp.flags & RT_FLAG_EXACT_BVH) != 0u;
     hipStream_t st = (hipStream_t)stream;
@@ -2247,8 +2296,12 @@ int rt_render_launch(rt_scene_handle s, const rt_camera_desc* camera, const rt_r
             hipLaunchKernelGGL(trace_samples<1>, dim3(grid_ref), dim3(64), lds_ref, st, dev_ref, cam, dp, q,
                                s->sbuf, s->counter, s->replay, 0u, d_segments);
         } else {  // fast kernel, then the reference kernel on the samples it handed over
-            hipLaunchKernelGGL(trace_samples<0>, dim3(grid), dim3(64), lds, st, s->dev, cam, dp, q, s->sbuf,
-                               s->counter, s->replay, 0u, d_segments);
+            if (s->fast_waves == 4)
+                hipLaunchKernelGGL((trace_samples<0, 4>), dim3(grid), dim3(64), lds, st, s->dev, cam, dp, q, s->sbuf,
+                                   s->counter, s->replay, 0u, d_segments);
+            else
+                hipLaunchKernelGGL((trace_samples<0, 3>), dim3(grid), dim3(64), lds, st, s->dev, cam, dp, q, s->sbuf,
+                                   s->counter, s->replay, 0u, d_segments);
             hipLaunchKernelGGL(trace_samples<1>, dim3(grid_ref), dim3(64), lds_ref, st, dev_ref, cam, dp, q,
                                s->sbuf, s->counter, s->replay, 1u, d_segments);
         }
