@@ -63,7 +63,8 @@ enum ProfRegion : uint32_t {
 };
 // traversal mode bits (bvh_hit): kModeExact = RT_FLAG_EXACT_BVH; the rest come
 // from DevParams::tune (RT_TUNE environment variable, diagnostics / A-B runs).
-constexpr uint32_t kModeExact = 1u, kModeNoLeafBoxes = 2u, kModeNoPermLds = 32u, kModeW3 = 64u;
+constexpr uint32_t kModeExact = 1u, kModeNoLeafBoxes = 2u, kModeNoPermLds = 32u, kModeW3 = 64u,
+                   kModeNoPretest = 128u;
 #ifdef RT_ABLATE
 // Ablation build (librtamd_ablate.so, diagnostics only): RT_TUNE bits that run a
 // piece of work twice (results of the copy discarded through an opaque test),
@@ -290,6 +291,24 @@ RT_DEV bool sphere_select(const Roots& R, float tmin, float tmax, float& t) {
     }
     t = (float)root;
     return true;
+}
+// f32 pretest of sphere.rs:57-68's f64 discriminant, for long top-level sphere runs.
+// Evaluated in f32 from the same f32 inputs, every rounding of half_b^2 - a * c
+// stays within 24 * 2^-24 * M of the exact value, M = half_b^2 + a * (|oc|^2 + r^2)
+// (Cauchy-Schwarz bounds each dot product by |oc| |d|), and the f64 evaluation
+// within ~2^-48 M of it. A value below -2^-16 M (256x that margin; M >= 2^-100 so
+// that underflow cannot matter) therefore proves the f64 discriminant negative:
+// the reference rejects the sphere (disc.is_sign_negative()). inf / NaN never reject.
+RT_DEV bool sphere_surely_missed(f4 s, const Ray& r) {
+    const float ocx = r.o.x - s.x, ocy = r.o.y - s.y, ocz = r.o.z - s.z;
+    const float a = (r.d.x * r.d.x + r.d.y * r.d.y) + r.d.z * r.d.z;
+    const float hb = (ocx * r.d.x + ocy * r.d.y) + ocz * r.d.z;
+    const float oc2 = (ocx * ocx + ocy * ocy) + ocz * ocz;
+    const float r2 = s.w * s.w;
+    const float hb2 = hb * hb;
+    const float disc = hb2 - a * (oc2 - r2);
+    const float m = hb2 + a * (oc2 + r2);
+    return m > 0x1p-100f && disc < -0x1p-16f * m;
 }
 // sphere.rs:49-103. Before dividing, spheres whose near root is certainly beyond
 // t_max, or whose far root is certainly before t_min, are rejected: with the
@@ -1101,10 +1120,18 @@ RT_DEV bool entry_geom_hit(const DevScene& S, float delta, const DevEntry* E, Ra
     if (E->kind == rtdev::kEntSphereRun) {  // consecutive top-level spheres, in list order
         const uint32_t first = E->payload, n = E->pad[0];
         const RayD q = to_d(r);
+        const bool pretest = n >= 8u && !(mode & kModeNoPretest);  // long lists (random_spheres without a BVH): most spheres are misses
         bool any = false;
         for (uint32_t i = 0; i < n; ++i) {
             float t;
-            if (sphere_t(ld4(S.sph + first + i), q, tmin, closest, t)) {
+            const f4 sp = ld4(S.sph + first + i);
+            if (pretest && sphere_surely_missed(sp, r)) {
+#ifdef RT_LEAF_AUDIT
+                if (sphere_roots(sp, q).ok) atomicAdd(&g_audit_count, 1u);  // audit: the f64 test must reject too
+#endif
+                continue;
+            }
+            if (sphere_t(sp, q, tmin, closest, t)) {
                 closest = t;
                 hit_code = rtdev::leaf_code(rtdev::kLeafSphere, first + i);
                 any = true;

@@ -251,3 +251,18 @@ def test_traversal_audit_full_c3_frame():
     out = r.stdout + r.stderr
     assert '{"leaf_audit_count": 0}' in out, out[-2000:]
     assert '{"trav_audit_count": 0}' in out, out[-2000:]
+
+
+def test_sphere_pretest_audit_c2():
+    # C2's 485-sphere list takes the f32 discriminant pretest; the audit build
+    # re-runs the f64 test on every pretest reject and counts any it would accept.
+    import subprocess
+    import sys
+    root = os.path.dirname(HERE)
+    lib = os.path.join(root, "raytracinginoneweekendinrust_amd", "_lib", "librtamd_audit.so")
+    env = dict(os.environ, RT_LIBRARY=lib)
+    r = subprocess.run([sys.executable, os.path.join(root, "tools", "region_profile.py"), "--config", "C2",
+                        "--spp", "16"], capture_output=True, text=True, env=env, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = r.stdout + r.stderr
+    assert '{"leaf_audit_count": 0}' in out, out[-2000:]
