@@ -1111,6 +1111,24 @@ RT_DEV Ray apply_op(f4 op, Ray r) {
     return r;
 }
 
+// sphere_surely_missed for two spheres at once (v_pk_mul_f32 / v_pk_add_f32: the
+// same rounded operations per element; the bound holds for any evaluation order).
+RT_DEV void spheres_surely_missed2(f4 s0, f4 s1, const Ray& r, float a, bool& m0, bool& m1) {
+    const pk2 ocx = pk(r.o.x, r.o.x) - pk(s0.x, s1.x), ocy = pk(r.o.y, r.o.y) - pk(s0.y, s1.y),
+              ocz = pk(r.o.z, r.o.z) - pk(s0.z, s1.z);
+    const pk2 dx = pk(r.d.x, r.d.x), dy = pk(r.d.y, r.d.y), dz = pk(r.d.z, r.d.z), a2 = pk(a, a);
+    const pk2 hb = (ocx * dx + ocy * dy) + ocz * dz;
+    const pk2 oc2 = (ocx * ocx + ocy * ocy) + ocz * ocz;
+    const pk2 rad = pk(s0.w, s1.w);
+    const pk2 r2 = rad * rad;
+    const pk2 hb2 = hb * hb;
+    const pk2 disc = hb2 - a2 * (oc2 - r2);
+    const pk2 m = hb2 + a2 * (oc2 + r2);
+    const pk2 lim = pk(-0x1p-16f, -0x1p-16f) * m;
+    m0 = m[0] > 0x1p-100f && disc[0] < lim[0];
+    m1 = m[1] > 0x1p-100f && disc[1] < lim[1];
+}
+
 // A GEOM or BVH entry (the caller guarantees E is wave-uniform).
 template <int kKind>
 RT_DEV bool entry_geom_hit(const DevScene& S, float delta, const DevEntry* E, Ray r, float tmin, float& closest,
@@ -1122,20 +1140,34 @@ RT_DEV bool entry_geom_hit(const DevScene& S, float delta, const DevEntry* E, Ra
         const RayD q = to_d(r);
         const bool pretest = n >= 8u && !(mode & kModeNoPretest);  // long lists (random_spheres without a BVH): most spheres are misses
         bool any = false;
-        for (uint32_t i = 0; i < n; ++i) {
+        auto test = [&](uint32_t i, f4 sp, bool missed) {  // sphere i in list order (hittable.rs:110-116)
             float t;
-            const f4 sp = ld4(S.sph + first + i);
-            if (pretest && sphere_surely_missed(sp, r)) {
+            if (missed) {
 #ifdef RT_LEAF_AUDIT
                 if (sphere_roots(sp, q).ok) atomicAdd(&g_audit_count, 1u);  // audit: the f64 test must reject too
 #endif
-                continue;
+                return;
             }
             if (sphere_t(sp, q, tmin, closest, t)) {
                 closest = t;
                 hit_code = rtdev::leaf_code(rtdev::kLeafSphere, first + i);
                 any = true;
             }
+        };
+        uint32_t i = 0;
+        if (pretest) {
+            const float a = (r.d.x * r.d.x + r.d.y * r.d.y) + r.d.z * r.d.z;
+            for (; i + 1u < n; i += 2u) {  // pairs: one packed pretest, then each sphere in order
+                const f4 s0 = ld4(S.sph + first + i), s1 = ld4(S.sph + first + i + 1u);
+                bool m0, m1;
+                spheres_surely_missed2(s0, s1, r, a, m0, m1);
+                test(i, s0, m0);
+                test(i + 1u, s1, m1);
+            }
+        }
+        for (; i < n; ++i) {
+            const f4 sp = ld4(S.sph + first + i);
+            test(i, sp, pretest && sphere_surely_missed(sp, r));
         }
         return any;
     }
