@@ -114,7 +114,7 @@ __device__ __forceinline__ void prof_add(uint32_t region, uint64_t t0) {
 #endif
 #ifdef RT_LEAF_AUDIT
 // Leaf-box audit (audit build, -DRT_LEAF_AUDIT -> librtamd_audit.so): leaves
-// rejected by leaf_box_may_hit are tested anyway; a rejected leaf that would have
+// rejected by the conservative leaf test are tested anyway; a rejected leaf that would have
 // produced a candidate is recorded here and printed when the scene is freed.
 struct LeafAudit {
     float o[3], d[3], tmin, closest, t, box[6], delta;
@@ -445,7 +445,7 @@ RT_DEV bool leaf_hit(const DevScene& S, uint32_t code, const Ray& r, const RayD&
         // The sides' axes are fixed (cube.rs:25-74: xy z0, xy z1, xz y0, xz y1,
         // yz x0, yz x1) and their bounds are the box's six values, read from the
         // records of sides 0 and 2: (z0, x0, x1, y0), y1 and (y0, x0, x1, z0), z1.
-        const f4 s0 = ld4(S.rect + 2 * idx), s2 = ld4(S.rect + 2 * idx + 4);
+        const f4 s0 = ld4(S.rect + 2 * idx);
         const float y1 = ld2(S.rect + 2 * idx + 1, 0).x, z1 = ld2(S.rect + 2 * idx + 5, 0).x;
         const float x0 = s0.y, x1 = s0.z, y0 = s0.w, z0 = s0.x;
         const float ox = r.o.x, oy = r.o.y, oz = r.o.z, dx = r.d.x, dy = r.d.y, dz = r.d.z;
@@ -514,40 +514,12 @@ RT_DEV bool slab(float x0, float y0, float z0, float x1, float y1, float z1, con
 // candidate inside it would then compute t > closest (exact pruning).
 RT_DEV float prune_bound(float closest) { return closest + __builtin_fabsf(closest) * 0x1p-19f; }
 
-// Conservative leaf test (prunable BVHs only): false only when the leaf's
-// primitive provably has no hit in [tmin, closest]. The box is the primitive's
-// own bounding box inflated by delta; any computed hit t lies on the ray within
-// rounding distance (<< delta) of that box, and the slab values carry <= 3
-// relative roundings, so the 2^-19 slacks below cover them ("exact
-// pruning"). NaN slab values (0 * inf) never reject.
-RT_DEV bool leaf_box_may_hit(float x0, float y0, float z0, float x1, float y1, float z1, const Ray& r, V inv,
-                             float tmin, float closest, float delta) {
-    float lo = -kInf, hi = kInf;
-    {
-        float a = ((x0 - delta) - r.o.x) * inv.x, b = ((x1 + delta) - r.o.x) * inv.x;
-        bool sw = inv.x < 0.0f;
-        float n = sw ? b : a, f = sw ? a : b;
-        lo = n > lo ? n : lo;
-        hi = f < hi ? f : hi;
-    }
-    {
-        float a = ((y0 - delta) - r.o.y) * inv.y, b = ((y1 + delta) - r.o.y) * inv.y;
-        bool sw = inv.y < 0.0f;
-        float n = sw ? b : a, f = sw ? a : b;
-        lo = n > lo ? n : lo;
-        hi = f < hi ? f : hi;
-    }
-    {
-        float a = ((z0 - delta) - r.o.z) * inv.z, b = ((z1 + delta) - r.o.z) * inv.z;
-        bool sw = inv.z < 0.0f;
-        float n = sw ? b : a, f = sw ? a : b;
-        lo = n > lo ? n : lo;
-        hi = f < hi ? f : hi;
-    }
-    if (lo > prune_bound(closest)) return false;
-    if (tmin > 0.0f && hi < tmin * (1.0f - 0x1p-19f)) return false;
-    return !(lo - hi > (__builtin_fabsf(lo) + __builtin_fabsf(hi)) * 0x1p-19f);
-}
+// Conservative leaf test (prunable BVHs only, leaf_intervals2 +
+// leaf_interval_may_hit): false only when the leaf's primitive provably has no hit
+// in [tmin, closest]. The box is the primitive's own bounding box inflated by
+// delta; any computed hit t lies on the ray within rounding distance (<< delta) of
+// that box, and the slab values carry <= 3 relative roundings, so the 2^-19
+// slacks cover them ("exact pruning").
 
 // Bvh::hit / BvhNode::hit (bvh.rs:212-217, 363-417) as an iterative traversal of
 // BVH2 nodes. Every child box gets the reference's own test (stored box, the
@@ -560,7 +532,7 @@ RT_DEV bool leaf_box_may_hit(float x0, float y0, float z0, float x1, float y1, f
 // nearest-first; ties resolve by DFS rank exactly like the recursion.
 // The stack lives in LDS, lane-strided: stack[level * 128 + {0, 64} + lane].
 #ifdef RT_LEAF_AUDIT
-// Leaf-box audit (audit build): a leaf rejected by leaf_box_may_hit is tested
+// Leaf-box audit (audit build): a leaf rejected by the conservative test is tested
 // anyway, and recorded if it would have produced a candidate.
 #define LEAF_AUDIT(CODE_, RANK_, X0_, Y0_, Z0_, X1_, Y1_, Z1_)                                          \
     do {                                                                                               \
@@ -794,7 +766,7 @@ RT_DEV bool bvh_hit_hrpp(const DevScene& S, uint32_t wrapper2, uint32_t pid, con
 // The returned key is what the stack keeps for the pop-time prune, so for a
 // prunable BVH it is always the conservative (inflated) entry, also while
 // closest is still infinite.
-RT_DEV float child_key(float x0, float y0, float z0, float x1, float y1, float z1, const Ray& r, V inv, float tmin,
+[[maybe_unused]] RT_DEV float child_key(float x0, float y0, float z0, float x1, float y1, float z1, const Ray& r, V inv, float tmin,
                        float tmax_entry, float closest, bool prune, float dmi) {
     float te;
     bool go = slab(x0, y0, z0, x1, y1, z1, r, inv, tmin, tmax_entry, te);
@@ -837,7 +809,7 @@ RT_DEV void child_keys4(f4 mnx, f4 mny, f4 mnz, f4 mxx, f4 mxy, f4 mxz, const Ra
     }
 }
 // The two leaf slots of a leaf node: the slab interval of each leaf's box
-// inflated by delta (leaf_box_may_hit's lo / hi), both leaves per packed
+// inflated by delta, both leaves per packed
 // instruction. The inflation is folded into shifted origins: x0 - (o + delta)
 // carries the same error structure as (x0 - delta) - o (one rounding of a
 // coordinate-sized value, <= 2^-24 R << delta, then relative roundings). NaN-free
@@ -860,7 +832,7 @@ RT_DEV void leaf_intervals2(float2 bx0, float2 by0, float2 bz0, float2 bx1, floa
         hi[e] = __builtin_fminf(__builtin_fminf(sx ? tax[e] : tbx[e], sy ? tay[e] : tby[e]), sz ? taz[e] : tbz[e]);
     }
 }
-// leaf_box_may_hit's decision on a precomputed inflated interval.
+// The conservative leaf test's decision on a precomputed inflated interval.
 RT_DEV bool leaf_interval_may_hit(float lo, float hi, float tmin, float closest) {
     if (lo > prune_bound(closest)) return false;
     if (tmin > 0.0f && hi < tmin * (1.0f - 0x1p-19f)) return false;
@@ -948,8 +920,8 @@ RT_DEV bool bvh_hit(const DevScene& S, float delta, uint32_t root, const Ray& r,
             if (leaf_boxes) leaf_intervals2(bx0, by0, bz0, bx1, by1, bz1, r, inv, delta, llo, lhi);
             for (uint32_t k = 0; k < nleaf; ++k) {
                 const uint32_t lcode = __float_as_uint(k ? chs.y : chs.x), rank = __float_as_uint(k ? rks.y : rks.x);
-                const float x0 = k ? bx0.y : bx0.x, y0 = k ? by0.y : by0.x, z0 = k ? bz0.y : bz0.x;
-                const float x1 = k ? bx1.y : bx1.x, y1 = k ? by1.y : by1.x, z1 = k ? bz1.y : bz1.x;
+                [[maybe_unused]] const float x0 = k ? bx0.y : bx0.x, y0 = k ? by0.y : by0.x, z0 = k ? bz0.y : bz0.x;
+                [[maybe_unused]] const float x1 = k ? bx1.y : bx1.x, y1 = k ? by1.y : by1.x, z1 = k ? bz1.y : bz1.x;
                 // the right leaf can only matter if t <= min(closest, left t)
                 const float bound = tmr < closest ? tmr : closest;
                 if (!leaf_boxes || leaf_interval_may_hit(k ? llo[1] : llo[0], k ? lhi[1] : lhi[0], tmin, bound)) {
@@ -2320,7 +2292,7 @@ int rt_render_launch(rt_scene_handle s, const rt_camera_desc* camera, const rt_r
             cus = 256;
         s->grid = per_cu * cus;
         s->grid_ref = per_cu_ref * cus;
-        if (getenv("RT_REPLAY_LOG"))
+        if (getenv("RT_LAUNCH_LOG"))
             fprintf(stderr, "rt: trace_samples<0, %d>: %d waves/CU (LDS %zu B/wave), reference kernel %d waves/CU\n",
                     s->fast_waves, per_cu, lds, per_cu_ref);
     }
@@ -2365,7 +2337,7 @@ int rt_render_launch(rt_scene_handle s, const rt_camera_desc* camera, const rt_r
                                s->sbuf, s->counter, s->replay, 1u, d_segments);
         }
         if ((e = hipGetLastError()) != hipSuccess) return hip_fail(e, "trace_samples launch");
-        if (getenv("RT_REPLAY_LOG")) {  // diagnostics: samples the fast kernel handed to the reference kernel
+        if (getenv("RT_LAUNCH_LOG")) {  // diagnostics: samples the fast kernel handed to the reference kernel
             TraceCounters h{};
             if (hipMemcpyAsync(&h, s->counter, sizeof h, hipMemcpyDeviceToHost, st) == hipSuccess &&
                 hipStreamSynchronize(st) == hipSuccess)

@@ -1,6 +1,6 @@
 #!/usr/bin/env bash
 # A/B session on the GPU box: GPU parity tests, then render_once timings of one
-# config under several environments (RT_REPLAY_LOG=1 prints the samples the fast
+# config under several environments (RT_LAUNCH_LOG=1 prints the samples the fast
 # kernel handed to the reference kernel). A fault / abort / timeout stops it.
 # Usage: bash tools/ab_session.sh [tests|notests] CONFIG SPP VARIANT...
 #   VARIANT: comma-separated env assignments, e.g. RT_TUNE=16 or
@@ -33,6 +33,6 @@ fi
 i=0
 for T in "$@"; do
     i=$((i + 1))
-    run "ab_${CFG}_${i}" 300 env ${T//,/ } RT_REPLAY_LOG=1 python tools/render_once.py --config "$CFG" --spp "$SPP" --reps 2
+    run "ab_${CFG}_${i}" 300 env ${T//,/ } RT_LAUNCH_LOG=1 python tools/render_once.py --config "$CFG" --spp "$SPP" --reps 2
 done
 echo "== ab done" | tee -a gpurun_out/ab_session.log
