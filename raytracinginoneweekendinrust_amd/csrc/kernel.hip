@@ -1101,8 +1101,11 @@ RT_DEV void spheres_surely_missed2(f4 s0, f4 s1, const Ray& r, float a, bool& m0
     m1 = m[1] > 0x1p-100f && disc[1] < lim[1];
 }
 
-// A GEOM or BVH entry (the caller guarantees E is wave-uniform).
-template <int kKind>
+constexpr uint32_t kRunPretestMin = 8u;  // sphere runs at least this long take the f32 pretest
+// A GEOM or BVH entry (the caller guarantees E is wave-uniform). kRuns: the kernel
+// instance carries the f32 pretest of long sphere runs (scenes that have such runs;
+// compiling it into the other instances costs them registers and speed).
+template <int kKind, bool kRuns>
 RT_DEV bool entry_geom_hit(const DevScene& S, float delta, const DevEntry* E, Ray r, float tmin, float& closest,
                            uint32_t& hit_code, uint32_t* stk, uint32_t mode, bool& replay) {
     uint32_t ntf = E->ntf;
@@ -1110,7 +1113,7 @@ RT_DEV bool entry_geom_hit(const DevScene& S, float delta, const DevEntry* E, Ra
     if (E->kind == rtdev::kEntSphereRun) {  // consecutive top-level spheres, in list order
         const uint32_t first = E->payload, n = E->pad[0];
         const RayD q = to_d(r);
-        const bool pretest = n >= 8u && !(mode & kModeNoPretest);  // long lists (random_spheres without a BVH): most spheres are misses
+        const bool pretest = kRuns && n >= kRunPretestMin && !(mode & kModeNoPretest);  // long lists (random_spheres without a BVH): most spheres are misses
         bool any = false;
         auto test = [&](uint32_t i, f4 sp, bool missed) {  // sphere i in list order (hittable.rs:110-116)
             float t;
@@ -1157,7 +1160,7 @@ RT_DEV bool entry_geom_hit(const DevScene& S, float delta, const DevEntry* E, Ra
 
 // ConstantMedium::hit (hittable.rs:176-233); draws one U(0,1) once the clamped
 // interval is non-empty, exactly where the reference does.
-template <int kKind>
+template <int kKind, bool kRuns>
 RT_DEV bool medium_hit(const DevScene& S, float delta, const DevEntry* E, Ray r, float tmin, float tmax, Rng& g,
                        const Key& k, float& t_out, uint32_t* stk, uint32_t mode, bool& replay) {
     uint32_t ntf = E->ntf;
@@ -1177,8 +1180,8 @@ RT_DEV bool medium_hit(const DevScene& S, float delta, const DevEntry* E, Ray r,
         if (!sphere_select(R, t1 + 0.0001f, kInf, t2)) return false;
     } else {
         uint32_t dummy;
-        if (!entry_geom_hit<kKind>(S, delta, B, r, -kInf, t1, dummy, stk, mode, replay)) return false;
-        if (!entry_geom_hit<kKind>(S, delta, B, r, t1 + 0.0001f, t2, dummy, stk, mode, replay)) return false;
+        if (!entry_geom_hit<kKind, kRuns>(S, delta, B, r, -kInf, t1, dummy, stk, mode, replay)) return false;
+        if (!entry_geom_hit<kKind, kRuns>(S, delta, B, r, t1 + 0.0001f, t2, dummy, stk, mode, replay)) return false;
     }
     if (t1 < tmin) t1 = tmin;
     if (t2 > tmax) t2 = tmax;
@@ -1513,7 +1516,7 @@ struct ChunkParams {
 };
 
 // HittableList::hit over the world (hittable.rs:100-118), t in [0.001, inf).
-template <int kKind>
+template <int kKind, bool kRuns>
 RT_DEV bool world_hit(const DevScene& S, float delta, const Ray& r, Rng& g, const Key& k, float& t_hit,
                       uint32_t& hit_entry, uint32_t& hit_code, uint32_t* stk, uint32_t mode, bool& replay) {
     float closest = kInf;
@@ -1523,7 +1526,7 @@ RT_DEV bool world_hit(const DevScene& S, float delta, const Ray& r, Rng& g, cons
         PROF_T0(pe);
         if (E->kind == rtdev::kEntMedium) {
             float t;
-            if (medium_hit<kKind>(S, delta, E, r, 0.001f, closest, g, k, t, stk, mode, replay)) {
+            if (medium_hit<kKind, kRuns>(S, delta, E, r, 0.001f, closest, g, k, t, stk, mode, replay)) {
                 closest = t;
                 hit_entry = e;
                 hit_code = rtdev::leaf_code(rtdev::kLeafMedium, 0);
@@ -1531,7 +1534,7 @@ RT_DEV bool world_hit(const DevScene& S, float delta, const Ray& r, Rng& g, cons
             }
         } else {
             uint32_t code;
-            if (entry_geom_hit<kKind>(S, delta, E, r, 0.001f, closest, code, stk, mode, replay)) {
+            if (entry_geom_hit<kKind, kRuns>(S, delta, E, r, 0.001f, closest, code, stk, mode, replay)) {
                 hit_entry = e;
                 hit_code = code;
                 any = true;
@@ -1695,7 +1698,7 @@ constexpr uint32_t kReplayCap = 1u << 20;
 // kWaves: the waves per SIMD the register allocator must allow. 3 (<= 168 VGPRs)
 // is the default; the fast kernel also exists at 4 (<= 128 VGPRs, a few spills),
 // launched when the scene's LDS stack fits four waves per SIMD (rt_render_launch).
-template <int kKind, int kWaves = 3>
+template <int kKind, int kWaves = 3, bool kRuns = true>
 __global__ __launch_bounds__(64, kWaves) void trace_samples(DevScene Sg, DevCamera C, DevParams P, ChunkParams Q,
                                                     float* __restrict__ sbuf, TraceCounters* __restrict__ ctr,
                                                     ReplayItem* __restrict__ replay_list, uint32_t fixup,
@@ -1763,7 +1766,7 @@ __global__ __launch_bounds__(64, kWaves) void trace_samples(DevScene Sg, DevCame
             uint32_t he = 0, hc = 0;
             bool replay = false;
             PROF_T0(pw);
-            bool any = world_hit<kKind>(S, P.prune_delta, ray, g, k, t, he, hc, stk, mode, replay);
+            bool any = world_hit<kKind, kRuns>(S, P.prune_delta, ray, g, k, t, he, hc, stk, mode, replay);
             PROF_ADD(kPrWorld, pw);
             if (kKind == 0 && replay) {  // hand the sample to the reference kernel
                 unsigned idx = atomicAdd(&ctr->replay_count, 1u);
@@ -1877,7 +1880,8 @@ struct rt_scene {
     TraceCounters* counter = nullptr;
     uint32_t stack_ref = 1;  // LDS stack entries per lane of trace_samples<1, 2> (dev.stack_depth: <0>)
     int grid = 0, grid_ref = 0;  // resident waves of trace_samples<0> / <1>
-    int fast_waves = 0;          // 3 or 4: the trace_samples<0, kWaves> instance this scene launches
+    int fast_waves = 0;          // 3 or 4: the trace_samples<0, kWaves, kRuns> instance this scene launches
+    bool long_runs = false;      // a top-level run of >= 8 spheres: the instance with the run pretest (kRuns)
     ReplayItem* replay = nullptr;  // kReplayCap entries
     float coord_bound = 0.0f;
     // HRPP experiment: tables (allocated at the first RT_FLAG_HRPP render) and counters
@@ -2044,6 +2048,8 @@ int rt_scene_upload(const rt_scene_desc* desc, int device, rt_scene_handle* out)
     d.hrpp_nkeys = (uint32_t)hs.hrpp_keys.size();
     d.hrpp_npred = hs.num_predictors;
     s->coord_bound = hs.coord_bound;
+    for (uint32_t e = 0; e < hs.num_top; ++e)
+        if (hs.entries[e].kind == rtdev::kEntSphereRun && hs.entries[e].pad[0] >= kRunPretestMin) s->long_runs = true;
     uint64_t c[10] = {hs.entries.size(), hs.sph.size(), hs.msph.size() / 3, hs.rect.size() / 2, hs.tri.size() / 3,
                       hs.nodes.size() / rtdev::kBvhNodeF4, hs.mats.size(), hs.texs.size(), hs.max_bvh_depth, total};
     memcpy(s->counts, c, sizeof c);
@@ -2239,10 +2245,10 @@ int rt_render_launch(rt_scene_handle s, const rt_camera_desc* camera, const rt_r
         const size_t stack_lds = (size_t)s->dev.stack_depth * 128u * sizeof(uint32_t);
         const size_t perm3 = s->dev.perm_bytes != 0u && s->dev.perm_bytes <= kPermLdsMax ? s->dev.perm_bytes : 0u;
         int per3 = 0, per4 = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per3, trace_samples<0, 3>, 64, stack_lds + perm3) != hipSuccess)
-            per3 = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per4, trace_samples<0, 4>, 64, stack_lds) != hipSuccess)
-            per4 = 0;
+        const auto k3 = s->long_runs ? trace_samples<0, 3, true> : trace_samples<0, 3, false>;
+        const auto k4 = s->long_runs ? trace_samples<0, 4, true> : trace_samples<0, 4, false>;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per3, k3, 64, stack_lds + perm3) != hipSuccess) per3 = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per4, k4, 64, stack_lds) != hipSuccess) per4 = 0;
         s->fast_waves = per4 > per3 && !(dp.tune & kModeW3) ? 4 : 3;
     }
     if (s->fast_waves == 4) dp.tune |= kModeNoPermLds;
@@ -2280,9 +2286,9 @@ int rt_render_launch(rt_scene_handle s, const rt_camera_desc* camera, const rt_r
     }
     if (s->grid == 0) {
         int per_cu = 0, per_cu_ref = 0, cus = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, s->fast_waves == 4 ? trace_samples<0, 4>
-                                                                                      : trace_samples<0, 3>,
-                                                         64, lds) != hipSuccess ||
+        const auto kf = s->fast_waves == 4 ? (s->long_runs ? trace_samples<0, 4, true> : trace_samples<0, 4, false>)
+                                           : (s->long_runs ? trace_samples<0, 3, true> : trace_samples<0, 3, false>);
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kf, 64, lds) != hipSuccess ||
             per_cu < 1)
             per_cu = 8;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_ref, trace_samples<1>, 64, lds_ref) != hipSuccess ||
@@ -2293,8 +2299,8 @@ int rt_render_launch(rt_scene_handle s, const rt_camera_desc* camera, const rt_r
         s->grid = per_cu * cus;
         s->grid_ref = per_cu_ref * cus;
         if (getenv("RT_LAUNCH_LOG"))
-            fprintf(stderr, "rt: trace_samples<0, %d>: %d waves/CU (LDS %zu B/wave), reference kernel %d waves/CU\n",
-                    s->fast_waves, per_cu, lds, per_cu_ref);
+            fprintf(stderr, "rt: trace_samples<0, %d, %s>: %d waves/CU (LDS %zu B/wave), reference kernel %d waves/CU\n",
+                    s->fast_waves, s->long_runs ? "runs" : "no runs", per_cu, lds, per_cu_ref);
     }
     const bool exact = (dp.flags & RT_FLAG_EXACT_BVH) != 0u;
     hipStream_t st = (hipStream_t)stream;
@@ -2327,12 +2333,11 @@ int rt_render_launch(rt_scene_handle s, const rt_camera_desc* camera, const rt_r
             hipLaunchKernelGGL(trace_samples<1>, dim3(grid_ref), dim3(64), lds_ref, st, dev_ref, cam, dp, q,
                                s->sbuf, s->counter, s->replay, 0u, d_segments);
         } else {  // fast kernel, then the reference kernel on the samples it handed over
-            if (s->fast_waves == 4)
-                hipLaunchKernelGGL((trace_samples<0, 4>), dim3(grid), dim3(64), lds, st, s->dev, cam, dp, q, s->sbuf,
-                                   s->counter, s->replay, 0u, d_segments);
-            else
-                hipLaunchKernelGGL((trace_samples<0, 3>), dim3(grid), dim3(64), lds, st, s->dev, cam, dp, q, s->sbuf,
-                                   s->counter, s->replay, 0u, d_segments);
+            const auto kf = s->fast_waves == 4
+                                ? (s->long_runs ? trace_samples<0, 4, true> : trace_samples<0, 4, false>)
+                                : (s->long_runs ? trace_samples<0, 3, true> : trace_samples<0, 3, false>);
+            hipLaunchKernelGGL(kf, dim3(grid), dim3(64), lds, st, s->dev, cam, dp, q, s->sbuf, s->counter, s->replay,
+                               0u, d_segments);
             hipLaunchKernelGGL(trace_samples<1>, dim3(grid_ref), dim3(64), lds_ref, st, dev_ref, cam, dp, q,
                                s->sbuf, s->counter, s->replay, 1u, d_segments);
         }
