@@ -419,8 +419,14 @@ RT_DEV bool tri_t(f4 t0, f4 t1, f4 t2, const Ray& r, float tmin, float tmax, flo
     return true;
 }
 
+// Scene features a fast-kernel instance is compiled for (kF): code for features a
+// scene lacks is left out of its instance, since unused code still costs the
+// instance registers and speed (measured: a flat scene runs 13% faster without
+// the BVH code, showcase 2.5% faster without the triangle code).
+constexpr uint32_t kFBvh = 1u, kFTri = 2u, kFRuns = 4u, kFAll = 7u;
 // One leaf (primitive or cube). tmax = closest so far; a hit with t == closest is
 // accepted, so later candidates win ties exactly like hittable.rs:110-116.
+template <uint32_t kF = kFAll>
 RT_DEV bool leaf_hit(const DevScene& S, uint32_t code, const Ray& r, const RayD& q, float tmin, float& closest,
                      uint32_t& hit_code) {
     uint32_t type = rtdev::leaf_type(code), idx = rtdev::leaf_index(code);
@@ -460,7 +466,7 @@ RT_DEV bool leaf_hit(const DevScene& S, uint32_t code, const Ray& r, const RayD&
         if (any) hit_code = rtdev::leaf_code(rtdev::kLeafRect, idx + face);
         return any;
     }
-    if (type == rtdev::kLeafTri) {
+    if ((kF & kFTri) && type == rtdev::kLeafTri) {
         if (tri_t(ld4(S.tri + 3 * idx), ld4(S.tri + 3 * idx + 1), ld4(S.tri + 3 * idx + 2), r, tmin, closest, t)) {
             closest = t;
             hit_code = code;
@@ -853,7 +859,7 @@ RT_DEV void sort2(float& ta, uint32_t& ca, float& tb, uint32_t& cb) {  // branch
 // to an axis plane (a zero direction component) gets t = (k - o) / d = 0 / 0 from
 // a rect whose plane holds its origin, and every comparison against NaN passes
 // (rectangle.rs:36-65); its sample is re-traced by the reference kernel.
-template <int kKind>
+template <int kKind, uint32_t kF = kFAll>
 RT_DEV bool bvh_hit(const DevScene& S, float delta, uint32_t root, const Ray& r, float tmin, float& closest,
                     uint32_t& hit_code, uint32_t* stk, uint32_t mode, bool& replay) {
     PROF_T0(pcall);
@@ -935,8 +941,8 @@ RT_DEV bool bvh_hit(const DevScene& S, float delta, uint32_t root, const Ray& r,
                     uint32_t code = 0u;
                     const RayD q = to_d(r);  // f64 ray for sphere leaves, rebuilt here rather than kept live
                     ABLATE(kAbLeaf2, float c2 = c; uint32_t h2 = 0u;
-                           if (leaf_hit(S, lcode, r, q, tmin, c2, h2) && h2 == 0x7fffffffu) c = -1.0f;);
-                    if (leaf_hit(S, lcode, r, q, tmin, c, code)) {
+                           if (leaf_hit<kF>(S, lcode, r, q, tmin, c2, h2) && h2 == 0x7fffffffu) c = -1.0f;);
+                    if (leaf_hit<kF>(S, lcode, r, q, tmin, c, code)) {
                         // cube faces rank + 0..5 (the face leaf_hit's list walk kept)
                         const uint32_t rk = rank + (rtdev::leaf_type(lcode) == rtdev::kLeafCube
                                                         ? rtdev::leaf_index(code) - rtdev::leaf_index(lcode)
@@ -1102,10 +1108,10 @@ RT_DEV void spheres_surely_missed2(f4 s0, f4 s1, const Ray& r, float a, bool& m0
 }
 
 constexpr uint32_t kRunPretestMin = 8u;  // sphere runs at least this long take the f32 pretest
-// A GEOM or BVH entry (the caller guarantees E is wave-uniform). kRuns: the kernel
-// instance carries the f32 pretest of long sphere runs (scenes that have such runs;
-// compiling it into the other instances costs them registers and speed).
-template <int kKind, bool kRuns>
+// A GEOM or BVH entry (the caller guarantees E is wave-uniform). Only instances
+// with kFRuns carry the f32 pretest of long sphere runs, only those with kFBvh the
+// BVH traversal (the host launches an instance whose features cover the scene's).
+template <int kKind, uint32_t kF>
 RT_DEV bool entry_geom_hit(const DevScene& S, float delta, const DevEntry* E, Ray r, float tmin, float& closest,
                            uint32_t& hit_code, uint32_t* stk, uint32_t mode, bool& replay) {
     uint32_t ntf = E->ntf;
@@ -1113,7 +1119,7 @@ RT_DEV bool entry_geom_hit(const DevScene& S, float delta, const DevEntry* E, Ra
     if (E->kind == rtdev::kEntSphereRun) {  // consecutive top-level spheres, in list order
         const uint32_t first = E->payload, n = E->pad[0];
         const RayD q = to_d(r);
-        const bool pretest = kRuns && n >= kRunPretestMin && !(mode & kModeNoPretest);  // long lists (random_spheres without a BVH): most spheres are misses
+        const bool pretest = (kF & kFRuns) && n >= kRunPretestMin && !(mode & kModeNoPretest);  // long lists (random_spheres without a BVH): most spheres are misses
         bool any = false;
         auto test = [&](uint32_t i, f4 sp, bool missed) {  // sphere i in list order (hittable.rs:110-116)
             float t;
@@ -1147,20 +1153,24 @@ RT_DEV bool entry_geom_hit(const DevScene& S, float delta, const DevEntry* E, Ra
         return any;
     }
     if (E->kind == rtdev::kEntBvh) {
-        ABLATE(kAbBvh2, float c2 = closest; uint32_t h2 = 0u; bool rp = false;
-               if (bvh_hit<kKind>(S, delta, E->payload, r, tmin, c2, h2, stk, mode, rp) && h2 == 0x7fffffffu)
-                   closest = -1.0f;);
-        return bvh_hit<kKind>(S, delta, E->payload, r, tmin, closest, hit_code, stk, mode, replay);
+        if constexpr ((kF & kFBvh) == 0u) {
+            return false;  // not reached: the scene has no BVH
+        } else {
+            ABLATE(kAbBvh2, float c2 = closest; uint32_t h2 = 0u; bool rp = false;
+                   if (bvh_hit<kKind, kF>(S, delta, E->payload, r, tmin, c2, h2, stk, mode, rp) && h2 == 0x7fffffffu)
+                       closest = -1.0f;);
+            return bvh_hit<kKind, kF>(S, delta, E->payload, r, tmin, closest, hit_code, stk, mode, replay);
+        }
     }
     RayD q = to_d(r);
     ABLATE(kAbGeom2, float c2 = closest; uint32_t h2 = 0u;
-           if (leaf_hit(S, E->payload, r, q, tmin, c2, h2) && h2 == 0x7fffffffu) closest = -1.0f;);
-    return leaf_hit(S, E->payload, r, q, tmin, closest, hit_code);
+           if (leaf_hit<kF>(S, E->payload, r, q, tmin, c2, h2) && h2 == 0x7fffffffu) closest = -1.0f;);
+    return leaf_hit<kF>(S, E->payload, r, q, tmin, closest, hit_code);
 }
 
 // ConstantMedium::hit (hittable.rs:176-233); draws one U(0,1) once the clamped
 // interval is non-empty, exactly where the reference does.
-template <int kKind, bool kRuns>
+template <int kKind, uint32_t kF>
 RT_DEV bool medium_hit(const DevScene& S, float delta, const DevEntry* E, Ray r, float tmin, float tmax, Rng& g,
                        const Key& k, float& t_out, uint32_t* stk, uint32_t mode, bool& replay) {
     uint32_t ntf = E->ntf;
@@ -1180,8 +1190,8 @@ RT_DEV bool medium_hit(const DevScene& S, float delta, const DevEntry* E, Ray r,
         if (!sphere_select(R, t1 + 0.0001f, kInf, t2)) return false;
     } else {
         uint32_t dummy;
-        if (!entry_geom_hit<kKind, kRuns>(S, delta, B, r, -kInf, t1, dummy, stk, mode, replay)) return false;
-        if (!entry_geom_hit<kKind, kRuns>(S, delta, B, r, t1 + 0.0001f, t2, dummy, stk, mode, replay)) return false;
+        if (!entry_geom_hit<kKind, kF>(S, delta, B, r, -kInf, t1, dummy, stk, mode, replay)) return false;
+        if (!entry_geom_hit<kKind, kF>(S, delta, B, r, t1 + 0.0001f, t2, dummy, stk, mode, replay)) return false;
     }
     if (t1 < tmin) t1 = tmin;
     if (t2 > tmax) t2 = tmax;
@@ -1226,6 +1236,7 @@ RT_DEV void rec_new(Rec& rec, const Ray& r, V outward, float t, float u, float v
 // (u, v) are computed only when the material reads them (kMatNeedsUV): they have
 // no side effects, so skipping them elsewhere changes no bit of the output.
 RT_DEV bool needs_uv(const DevScene& S, uint32_t mat) { return (S.mats[mat].flags & rtdev::kMatNeedsUV) != 0u; }
+template <uint32_t kF = kFAll>
 RT_DEV void prim_record(const DevScene& S, uint32_t code, const Ray& r, float t, Rec& rec) {
     uint32_t type = rtdev::leaf_type(code), idx = rtdev::leaf_index(code);
     float u = 0.0f, v = 0.0f;
@@ -1248,7 +1259,7 @@ RT_DEV void prim_record(const DevScene& S, uint32_t code, const Ray& r, float t,
         }
         V n = axis == 0u ? mk(0.0f, 0.0f, 1.0f) : (axis == 1u ? mk(0.0f, 1.0f, 0.0f) : mk(1.0f, 0.0f, 0.0f));
         rec_new(rec, r, n, t, u, v, mat);
-    } else if (type == rtdev::kLeafTri) {
+    } else if ((kF & kFTri) && type == rtdev::kLeafTri) {
         f4 t0 = ld4(S.tri + 3 * idx), t1 = ld4(S.tri + 3 * idx + 1), t2 = ld4(S.tri + 3 * idx + 2);
         V n = normalize(cross(xyz(t1), xyz(t2)));
         rec_new(rec, r, n, t, 0.0f, 0.0f, __float_as_uint(t0.w));
@@ -1261,6 +1272,7 @@ RT_DEV void prim_record(const DevScene& S, uint32_t code, const Ray& r, float t,
         rec_new(rec, r, n, t, u, v, mat);
     }
 }
+template <uint32_t kF = kFAll>
 RT_DEV void make_record(const DevScene& S, uint32_t entry, uint32_t code, float t, const Ray& r0, Rec& rec) {
     const DevEntry* E = S.entries + entry;
     uint32_t ntf = E->ntf;
@@ -1277,7 +1289,7 @@ RT_DEV void make_record(const DevScene& S, uint32_t entry, uint32_t code, float 
         rec.front = true;
         rec.mat = E->phase_mat;
     } else {
-        prim_record(S, code, r3, t, rec);
+        prim_record<kF>(S, code, r3, t, rec);
     }
     // unwind the chain inner -> outer (instance.rs:41, 128-140)
 #pragma unroll
@@ -1516,7 +1528,7 @@ struct ChunkParams {
 };
 
 // HittableList::hit over the world (hittable.rs:100-118), t in [0.001, inf).
-template <int kKind, bool kRuns>
+template <int kKind, uint32_t kF>
 RT_DEV bool world_hit(const DevScene& S, float delta, const Ray& r, Rng& g, const Key& k, float& t_hit,
                       uint32_t& hit_entry, uint32_t& hit_code, uint32_t* stk, uint32_t mode, bool& replay) {
     float closest = kInf;
@@ -1526,7 +1538,7 @@ RT_DEV bool world_hit(const DevScene& S, float delta, const Ray& r, Rng& g, cons
         PROF_T0(pe);
         if (E->kind == rtdev::kEntMedium) {
             float t;
-            if (medium_hit<kKind, kRuns>(S, delta, E, r, 0.001f, closest, g, k, t, stk, mode, replay)) {
+            if (medium_hit<kKind, kF>(S, delta, E, r, 0.001f, closest, g, k, t, stk, mode, replay)) {
                 closest = t;
                 hit_entry = e;
                 hit_code = rtdev::leaf_code(rtdev::kLeafMedium, 0);
@@ -1534,7 +1546,7 @@ RT_DEV bool world_hit(const DevScene& S, float delta, const Ray& r, Rng& g, cons
             }
         } else {
             uint32_t code;
-            if (entry_geom_hit<kKind, kRuns>(S, delta, E, r, 0.001f, closest, code, stk, mode, replay)) {
+            if (entry_geom_hit<kKind, kF>(S, delta, E, r, 0.001f, closest, code, stk, mode, replay)) {
                 hit_entry = e;
                 hit_code = code;
                 any = true;
@@ -1639,6 +1651,7 @@ RT_DEV bool take_sample(ItemPool& pool, bool want, const DevCamera& C, const Dev
 // The end of a segment whose list walk is complete (ray.rs:43-61): background,
 // or HitRecord + emit + scatter. Returns true when the path ends; its radiance is
 // then stored in the sample buffer.
+template <uint32_t kF = kFAll>
 RT_DEV bool finish_segment(const DevScene& S, const DevParams& P, const ChunkParams& Q, const Key& k,
                            float* __restrict__ sbuf, bool any, uint32_t he, uint32_t hc, float t, Ray& ray, V& L, V& T,
                            uint32_t& depth, Rng& g, uint32_t pixel, uint32_t s_local) {
@@ -1650,7 +1663,7 @@ RT_DEV bool finish_segment(const DevScene& S, const DevParams& P, const ChunkPar
     } else {
         Rec rec;
         PROF_T0(pc);
-        make_record(S, he, hc, t, ray, rec);
+        make_record<kF>(S, he, hc, t, ray, rec);
         PROF_ADD(kPrRecord, pc);
         const DevMaterial m = S.mats[rec.mat];
         PROF_T0(pm);
@@ -1698,7 +1711,7 @@ constexpr uint32_t kReplayCap = 1u << 20;
 // kWaves: the waves per SIMD the register allocator must allow. 3 (<= 168 VGPRs)
 // is the default; the fast kernel also exists at 4 (<= 128 VGPRs, a few spills),
 // launched when the scene's LDS stack fits four waves per SIMD (rt_render_launch).
-template <int kKind, int kWaves = 3, bool kRuns = true>
+template <int kKind, int kWaves = 3, uint32_t kF = kFAll>
 __global__ __launch_bounds__(64, kWaves) void trace_samples(DevScene Sg, DevCamera C, DevParams P, ChunkParams Q,
                                                     float* __restrict__ sbuf, TraceCounters* __restrict__ ctr,
                                                     ReplayItem* __restrict__ replay_list, uint32_t fixup,
@@ -1766,13 +1779,13 @@ __global__ __launch_bounds__(64, kWaves) void trace_samples(DevScene Sg, DevCame
             uint32_t he = 0, hc = 0;
             bool replay = false;
             PROF_T0(pw);
-            bool any = world_hit<kKind, kRuns>(S, P.prune_delta, ray, g, k, t, he, hc, stk, mode, replay);
+            bool any = world_hit<kKind, kF>(S, P.prune_delta, ray, g, k, t, he, hc, stk, mode, replay);
             PROF_ADD(kPrWorld, pw);
             if (kKind == 0 && replay) {  // hand the sample to the reference kernel
                 unsigned idx = atomicAdd(&ctr->replay_count, 1u);
                 if (idx < kReplayCap) replay_list[idx] = ReplayItem{pixel, s_local};
                 has = false;
-            } else if (finish_segment(S, P, Q, k, sbuf, any, he, hc, t, ray, L, T, depth, g, pixel, s_local)) {
+            } else if (finish_segment<kF>(S, P, Q, k, sbuf, any, he, hc, t, ray, L, T, depth, g, pixel, s_local)) {
                 has = false;
                 nseg += nseg_sample;
             }
@@ -1880,8 +1893,8 @@ struct rt_scene {
     TraceCounters* counter = nullptr;
     uint32_t stack_ref = 1;  // LDS stack entries per lane of trace_samples<1, 2> (dev.stack_depth: <0>)
     int grid = 0, grid_ref = 0;  // resident waves of trace_samples<0> / <1>
-    int fast_waves = 0;          // 3 or 4: the trace_samples<0, kWaves, kRuns> instance this scene launches
-    bool long_runs = false;      // a top-level run of >= 8 spheres: the instance with the run pretest (kRuns)
+    int fast_waves = 0;          // 3 or 4: the trace_samples<0, kWaves, kF> instance this scene launches
+    uint32_t features = kFAll;   // kF bits the scene needs (BVHs, triangles, long sphere runs)
     ReplayItem* replay = nullptr;  // kReplayCap entries
     float coord_bound = 0.0f;
     // HRPP experiment: tables (allocated at the first RT_FLAG_HRPP render) and counters
@@ -1913,6 +1926,23 @@ struct DeviceGuard {  // restores the caller's current device (e.g. torch's)
         if (prev >= 0) (void)hipSetDevice(prev);
     }
 };
+
+// The fast-kernel instance for a scene: the first feature preset that covers the
+// scene's features (flat lists; flat lists with long sphere runs; BVHs without
+// triangles; BVHs with triangles; everything).
+using TraceKernel = void (*)(DevScene, DevCamera, DevParams, ChunkParams, float*, TraceCounters*, ReplayItem*, uint32_t,
+                             unsigned long long*);
+template <int kWaves>
+TraceKernel fast_instance(uint32_t features) {
+    if (features == 0u) return trace_samples<0, kWaves, 0u>;
+    if ((features & ~kFRuns) == 0u) return trace_samples<0, kWaves, kFRuns>;
+    if ((features & ~kFBvh) == 0u) return trace_samples<0, kWaves, kFBvh>;
+    if ((features & ~(kFBvh | kFTri)) == 0u) return trace_samples<0, kWaves, kFBvh | kFTri>;
+    return trace_samples<0, kWaves, kFAll>;
+}
+TraceKernel fast_instance(int waves, uint32_t features) {
+    return waves == 4 ? fast_instance<4>(features) : fast_instance<3>(features);
+}
 
 int check_device(int device) {
     int n = 0;
@@ -2048,8 +2078,11 @@ int rt_scene_upload(const rt_scene_desc* desc, int device, rt_scene_handle* out)
     d.hrpp_nkeys = (uint32_t)hs.hrpp_keys.size();
     d.hrpp_npred = hs.num_predictors;
     s->coord_bound = hs.coord_bound;
-    for (uint32_t e = 0; e < hs.num_top; ++e)
-        if (hs.entries[e].kind == rtdev::kEntSphereRun && hs.entries[e].pad[0] >= kRunPretestMin) s->long_runs = true;
+    s->features = hs.tri.empty() ? 0u : kFTri;
+    for (const rtdev::DevEntry& e : hs.entries) {  // top-level entries and medium boundaries
+        if (e.kind == rtdev::kEntBvh) s->features |= kFBvh;
+        if (e.kind == rtdev::kEntSphereRun && e.pad[0] >= kRunPretestMin) s->features |= kFRuns;
+    }
     uint64_t c[10] = {hs.entries.size(), hs.sph.size(), hs.msph.size() / 3, hs.rect.size() / 2, hs.tri.size() / 3,
                       hs.nodes.size() / rtdev::kBvhNodeF4, hs.mats.size(), hs.texs.size(), hs.max_bvh_depth, total};
     memcpy(s->counts, c, sizeof c);
@@ -2245,8 +2278,7 @@ int rt_render_launch(rt_scene_handle s, const rt_camera_desc* camera, const rt_r
         const size_t stack_lds = (size_t)s->dev.stack_depth * 128u * sizeof(uint32_t);
         const size_t perm3 = s->dev.perm_bytes != 0u && s->dev.perm_bytes <= kPermLdsMax ? s->dev.perm_bytes : 0u;
         int per3 = 0, per4 = 0;
-        const auto k3 = s->long_runs ? trace_samples<0, 3, true> : trace_samples<0, 3, false>;
-        const auto k4 = s->long_runs ? trace_samples<0, 4, true> : trace_samples<0, 4, false>;
+        const TraceKernel k3 = fast_instance(3, s->features), k4 = fast_instance(4, s->features);
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per3, k3, 64, stack_lds + perm3) != hipSuccess) per3 = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per4, k4, 64, stack_lds) != hipSuccess) per4 = 0;
         s->fast_waves = per4 > per3 && !(dp.tune & kModeW3) ? 4 : 3;
@@ -2286,8 +2318,7 @@ int rt_render_launch(rt_scene_handle s, const rt_camera_desc* camera, const rt_r
     }
     if (s->grid == 0) {
         int per_cu = 0, per_cu_ref = 0, cus = 0;
-        const auto kf = s->fast_waves == 4 ? (s->long_runs ? trace_samples<0, 4, true> : trace_samples<0, 4, false>)
-                                           : (s->long_runs ? trace_samples<0, 3, true> : trace_samples<0, 3, false>);
+        const TraceKernel kf = fast_instance(s->fast_waves, s->features);
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kf, 64, lds) != hipSuccess ||
             per_cu < 1)
             per_cu = 8;
@@ -2299,8 +2330,8 @@ int rt_render_launch(rt_scene_handle s, const rt_camera_desc* camera, const rt_r
         s->grid = per_cu * cus;
         s->grid_ref = per_cu_ref * cus;
         if (getenv("RT_LAUNCH_LOG"))
-            fprintf(stderr, "rt: trace_samples<0, %d, %s>: %d waves/CU (LDS %zu B/wave), reference kernel %d waves/CU\n",
-                    s->fast_waves, s->long_runs ? "runs" : "no runs", per_cu, lds, per_cu_ref);
+            fprintf(stderr, "rt: trace_samples<0, %d, features 0x%x>: %d waves/CU (LDS %zu B/wave), reference kernel %d "
+                    "waves/CU\n", s->fast_waves, s->features, per_cu, lds, per_cu_ref);
     }
     const bool exact = (dp.flags & RT_FLAG_EXACT_BVH) != 0u;
     hipStream_t st = (hipStream_t)stream;
@@ -2333,9 +2364,7 @@ int rt_render_launch(rt_scene_handle s, const rt_camera_desc* camera, const rt_r
             hipLaunchKernelGGL(trace_samples<1>, dim3(grid_ref), dim3(64), lds_ref, st, dev_ref, cam, dp, q,
                                s->sbuf, s->counter, s->replay, 0u, d_segments);
         } else {  // fast kernel, then the reference kernel on the samples it handed over
-            const auto kf = s->fast_waves == 4
-                                ? (s->long_runs ? trace_samples<0, 4, true> : trace_samples<0, 4, false>)
-                                : (s->long_runs ? trace_samples<0, 3, true> : trace_samples<0, 3, false>);
+            const TraceKernel kf = fast_instance(s->fast_waves, s->features);
             hipLaunchKernelGGL(kf, dim3(grid), dim3(64), lds, st, s->dev, cam, dp, q, s->sbuf, s->counter, s->replay,
                                0u, d_segments);
             hipLaunchKernelGGL(trace_samples<1>, dim3(grid_ref), dim3(64), lds_ref, st, dev_ref, cam, dp, q,
