@@ -266,3 +266,30 @@ def test_sphere_pretest_audit_c2():
     assert r.returncode == 0, r.stderr[-2000:]
     out = r.stdout + r.stderr
     assert '{"leaf_audit_count": 0}' in out, out[-2000:]
+
+
+@pytest.mark.parametrize("with_tri", [False, True])
+def test_every_feature_preset_instance(with_tri, rt, orc):
+    # A long top-level sphere run (the f32 pretest), a BVH and, optionally, a
+    # triangle: the scene needs the all-features instance of the fast kernel
+    # (the flat / BVH-only presets are exercised by the C1-C5 cases above).
+    b = rt.SceneBuilder()
+    white = b.lambertian_from_color((0.7, 0.7, 0.7))
+    metal = b.metal((0.8, 0.6, 0.2), 0.1)
+    w = rt.HittableList()
+    for i in range(11):
+        w.add(b.sphere((i - 5.0, 0.3 * (i % 3), -1.0 - 0.2 * (i % 2)), 0.45, metal if i % 2 else white))
+    inner = rt.HittableList()
+    for i in range(12):
+        inner.add(b.sphere((i - 6.0, 1.6, 0.5 * (i % 4)), 0.35, white))
+    w.add(b.bvh(inner, 0.0, 1.0, axis_seed=5))
+    if with_tri:
+        w.add(b.tri((-6, -1, -3), (6, -1, -3), (0, 4, -3), white))
+    w.add(b.sphere((0, -1000.5, 0), 1000.0, white))
+    sc = b.finish(w)
+    cam = rt.Camera.new((0, 2, 9), (0, 0.5, 0), (0, 1, 0), 45.0, 1.5, 0.05, 9.0, 0.0, 0.0)
+    params = rt.render_params(36, 24, 4, 12, background=(0.6, 0.7, 0.9))
+    want, cnt = orc.render(sc, cam, params)
+    got, st = gpu_render(rt, sc, cam, params)
+    np.testing.assert_array_equal(got, want)
+    assert st["segments"] == cnt["segments"]
