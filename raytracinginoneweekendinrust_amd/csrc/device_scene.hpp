@@ -147,6 +147,10 @@ struct DevScene {
     unsigned long long* hrpp_stats;       // per predictor: tp, fp, np, dropped
     uint32_t* hrpp_cnt;                   // per-wave LDS counters (set in the kernel)
     uint32_t hrpp_bits, hrpp_nkeys, hrpp_npred, pad0;
+    // Deep BVHs (instances with kFDeep): stack entries past stack_depth live in HBM,
+    // stack_spill[((wave * spill_depth + entry - stack_depth) * 64 + lane) * 2 + {node, t}]
+    uint32_t* stack_spill;
+    uint32_t spill_depth, pad1;
 };
 
 // Camera::new (camera.rs:44-81) evaluated on the host.

@@ -423,7 +423,9 @@ RT_DEV bool tri_t(f4 t0, f4 t1, f4 t2, const Ray& r, float tmin, float tmax, flo
 // scene lacks is left out of its instance, since unused code still costs the
 // instance registers and speed (measured: a flat scene runs 13% faster without
 // the BVH code, showcase 2.5% faster without the triangle code).
-constexpr uint32_t kFBvh = 1u, kFTri = 2u, kFRuns = 4u, kFAll = 7u;
+constexpr uint32_t kFBvh = 1u, kFTri = 2u, kFRuns = 4u, kFDeep = 8u, kFAll = 15u;  // kFDeep: a BVH stack deeper
+                                                                                  // than kStackLdsMax entries
+[[maybe_unused]] constexpr uint32_t kStackLdsMax = 19u;  // LDS stack entries per lane at most (9.5 KB per wave: 16 waves/CU)
 // One leaf (primitive or cube). tmax = closest so far; a hit with t == closest is
 // accepted, so later candidates win ties exactly like hittable.rs:110-116.
 template <uint32_t kF = kFAll>
@@ -1001,22 +1003,23 @@ RT_DEV bool bvh_hit(const DevScene& S, float delta, uint32_t root, const Ray& r,
         sort2(t0, c0, t2, c2);
         sort2(t1, c1, t3, c3);
         sort2(t1, c1, t2, c2);
+        // LDS stack; with kFDeep the entries past stack_depth go to the HBM spill area
+        auto push = [&](uint32_t node, float t) {
+            if (!(kF & kFDeep) || sp < S.stack_depth) {
+                stk[sp * 128u] = node;
+                stk[sp * 128u + 64u] = __float_as_uint(t);
+            } else {
+                uint32_t* g = S.stack_spill +
+                              (((size_t)blockIdx.x * S.spill_depth + (sp - S.stack_depth)) * 64u + threadIdx.x) * 2u;
+                g[0] = node;
+                g[1] = __float_as_uint(t);
+            }
+            sp += 1u;
+        };
         if (t0 != kInf) {  // visit the nearest now, push the others far to near
-            if (t3 != kInf) {
-                stk[sp * 128u] = c3;
-                stk[sp * 128u + 64u] = __float_as_uint(t3);
-                sp += 1u;
-            }
-            if (t2 != kInf) {
-                stk[sp * 128u] = c2;
-                stk[sp * 128u + 64u] = __float_as_uint(t2);
-                sp += 1u;
-            }
-            if (t1 != kInf) {
-                stk[sp * 128u] = c1;
-                stk[sp * 128u + 64u] = __float_as_uint(t1);
-                sp += 1u;
-            }
+            if (t3 != kInf) push(c3, t3);
+            if (t2 != kInf) push(c2, t2);
+            if (t1 != kInf) push(c1, t1);
             cur = c0;
             PROF_ADD(kPrBvhPush, pp);
             continue;
@@ -1026,8 +1029,17 @@ RT_DEV bool bvh_hit(const DevScene& S, float delta, uint32_t root, const Ray& r,
         bool found = false;
         while (sp > 0u) {
             sp -= 1u;
-            uint32_t cand = stk[sp * 128u];
-            float tenter = __uint_as_float(stk[sp * 128u + 64u]);
+            uint32_t cand;
+            float tenter;
+            if (!(kF & kFDeep) || sp < S.stack_depth) {
+                cand = stk[sp * 128u];
+                tenter = __uint_as_float(stk[sp * 128u + 64u]);
+            } else {
+                const uint32_t* g = S.stack_spill +
+                                    (((size_t)blockIdx.x * S.spill_depth + (sp - S.stack_depth)) * 64u + threadIdx.x) * 2u;
+                cand = g[0];
+                tenter = __uint_as_float(g[1]);
+            }
             if (!prune || !(tenter > prune_bound(closest))) {
                 cur = cand;
                 found = true;
@@ -1894,7 +1906,8 @@ struct rt_scene {
     uint32_t stack_ref = 1;  // LDS stack entries per lane of trace_samples<1, 2> (dev.stack_depth: <0>)
     int grid = 0, grid_ref = 0;  // resident waves of trace_samples<0> / <1>
     int fast_waves = 0;          // 3 or 4: the trace_samples<0, kWaves, kF> instance this scene launches
-    uint32_t features = kFAll;   // kF bits the scene needs (BVHs, triangles, long sphere runs)
+    uint32_t features = kFAll;   // kF bits the scene needs (BVHs, triangles, long sphere runs, deep stacks)
+    uint32_t* stack_spill = nullptr;  // kFDeep: HBM stack entries past kStackLdsMax, grid x spill_depth x 64 x 2 words
     ReplayItem* replay = nullptr;  // kReplayCap entries
     float coord_bound = 0.0f;
     // HRPP experiment: tables (allocated at the first RT_FLAG_HRPP render) and counters
@@ -1929,7 +1942,7 @@ struct DeviceGuard {  // restores the caller's current device (e.g. torch's)
 
 // The fast-kernel instance for a scene: the first feature preset that covers the
 // scene's features (flat lists; flat lists with long sphere runs; BVHs without
-// triangles; BVHs with triangles; everything).
+// triangles; BVHs with triangles and deep stacks; everything).
 using TraceKernel = void (*)(DevScene, DevCamera, DevParams, ChunkParams, float*, TraceCounters*, ReplayItem*, uint32_t,
                              unsigned long long*);
 template <int kWaves>
@@ -1937,7 +1950,7 @@ TraceKernel fast_instance(uint32_t features) {
     if (features == 0u) return trace_samples<0, kWaves, 0u>;
     if ((features & ~kFRuns) == 0u) return trace_samples<0, kWaves, kFRuns>;
     if ((features & ~kFBvh) == 0u) return trace_samples<0, kWaves, kFBvh>;
-    if ((features & ~(kFBvh | kFTri)) == 0u) return trace_samples<0, kWaves, kFBvh | kFTri>;
+    if ((features & ~(kFBvh | kFTri | kFDeep)) == 0u) return trace_samples<0, kWaves, kFBvh | kFTri | kFDeep>;
     return trace_samples<0, kWaves, kFAll>;
 }
 TraceKernel fast_instance(int waves, uint32_t features) {
@@ -2079,6 +2092,18 @@ int rt_scene_upload(const rt_scene_desc* desc, int device, rt_scene_handle* out)
     d.hrpp_npred = hs.num_predictors;
     s->coord_bound = hs.coord_bound;
     s->features = hs.tri.empty() ? 0u : kFTri;
+#ifndef RT_LEAF_AUDIT  // (the audit build replays traversals on the same LDS stack: no spill area)
+    {  // deep BVHs: the LDS stack keeps kStackLdsMax entries, HBM the rest
+        uint32_t cap = kStackLdsMax;
+        if (const char* env = getenv("RT_STACK_LDS"))  // diagnostics / tests: a smaller LDS part (>= 1)
+            cap = std::max(1u, std::min(cap, (uint32_t)strtoul(env, nullptr, 10)));
+        if (hs.max_stack > cap) {
+            s->features |= kFDeep;
+            d.stack_depth = cap;
+            d.spill_depth = hs.max_stack - cap;
+        }
+    }
+#endif
     for (const rtdev::DevEntry& e : hs.entries) {  // top-level entries and medium boundaries
         if (e.kind == rtdev::kEntBvh) s->features |= kFBvh;
         if (e.kind == rtdev::kEntSphereRun && e.pad[0] >= kRunPretestMin) s->features |= kFRuns;
@@ -2143,6 +2168,7 @@ int rt_scene_free(rt_scene_handle s) {
         if (s->pool) (void)hipFree(s->pool);
         if (s->sbuf) (void)hipFree(s->sbuf);
         if (s->counter) (void)hipFree(s->counter);
+        if (s->stack_spill) (void)hipFree(s->stack_spill);
         if (s->replay) (void)hipFree(s->replay);
         if (s->hrpp_tab) (void)hipFree(s->hrpp_tab);
         if (s->hrpp_stats) (void)hipFree(s->hrpp_stats);
@@ -2329,6 +2355,14 @@ int rt_render_launch(rt_scene_handle s, const rt_camera_desc* camera, const rt_r
             cus = 256;
         s->grid = per_cu * cus;
         s->grid_ref = per_cu_ref * cus;
+        if (s->features & kFDeep) {  // the deep-stack spill area: one slab per resident wave
+            const size_t bytes = (size_t)s->grid * s->dev.spill_depth * 64u * 2u * sizeof(uint32_t);
+            if ((e = hipMalloc(&s->stack_spill, bytes)) != hipSuccess) {
+                s->grid = 0;
+                return rthost::set_error(RT_ERR_OOM, std::string("hipMalloc stack spill: ") + hipGetErrorString(e));
+            }
+            s->dev.stack_spill = s->stack_spill;
+        }
         if (getenv("RT_LAUNCH_LOG"))
             fprintf(stderr, "rt: trace_samples<0, %d, features 0x%x>: %d waves/CU (LDS %zu B/wave), reference kernel %d "
                     "waves/CU\n", s->fast_waves, s->features, per_cu, lds, per_cu_ref);

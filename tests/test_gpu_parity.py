@@ -293,3 +293,16 @@ def test_every_feature_preset_instance(with_tri, rt, orc):
     got, st = gpu_render(rt, sc, cam, params)
     np.testing.assert_array_equal(got, want)
     assert st["segments"] == cnt["segments"]
+
+
+@pytest.mark.parametrize("cfg_name", ["C3", "C4"])
+def test_stack_spill_to_hbm_matches_oracle(cfg_name, rt, orc, monkeypatch):
+    # Deep BVHs keep kStackLdsMax stack entries in LDS and the rest in HBM; a 2-entry
+    # LDS part (RT_STACK_LDS, read at upload) sends almost every traversal through
+    # the HBM half, on the pruned (C3) and the unpruned triangle (C4) traversal.
+    monkeypatch.setenv("RT_STACK_LDS", "2")
+    cfg, scene, params = setup(rt, cfg_name, 40, 2, seed=3)
+    want, cnt = orc.render(scene, cfg.camera(), params)
+    got, st = gpu_render(rt, scene, cfg.camera(), params)
+    np.testing.assert_array_equal(got, want)
+    assert st["segments"] == cnt["segments"]

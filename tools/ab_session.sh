@@ -1,7 +1,7 @@
 #!/usr/bin/env bash
 # A/B session on the GPU box: GPU parity tests, then render_once timings of one
-# config under several environments (RT_LAUNCH_LOG=1 prints the samples the fast
-# kernel handed to the reference kernel). A fault / abort / timeout stops it.
+# config under several environments (RT_LAUNCH_LOG=1 prints the launched instance
+# and its occupancy). A fault / abort / timeout stops it.
 # Usage: bash tools/ab_session.sh [tests|notests] CONFIG SPP VARIANT...
 #   VARIANT: comma-separated env assignments, e.g. RT_TUNE=16 or
 #            RT_LIBRARY=raytracinginoneweekendinrust_amd/_lib/librtamd_w3.so,RT_TUNE=0
