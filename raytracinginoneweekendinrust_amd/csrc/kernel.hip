@@ -423,8 +423,9 @@ RT_DEV bool tri_t(f4 t0, f4 t1, f4 t2, const Ray& r, float tmin, float tmax, flo
 // scene lacks is left out of its instance, since unused code still costs the
 // instance registers and speed (measured: a flat scene runs 13% faster without
 // the BVH code, showcase 2.5% faster without the triangle code).
-constexpr uint32_t kFBvh = 1u, kFTri = 2u, kFRuns = 4u, kFDeep = 8u, kFAll = 15u;  // kFDeep: a BVH stack deeper
-                                                                                  // than kStackLdsMax entries
+// kFDeep: a BVH stack deeper than kStackLdsMax entries; kFLeafRM: BVH leaves that are
+// rects or moving spheres (BVH leaf tests otherwise handle spheres, cubes, triangles).
+constexpr uint32_t kFBvh = 1u, kFTri = 2u, kFRuns = 4u, kFDeep = 8u, kFLeafRM = 16u, kFAll = 31u;
 [[maybe_unused]] constexpr uint32_t kStackLdsMax = 19u;  // LDS stack entries per lane at most (9.5 KB per wave: 16 waves/CU)
 // One leaf (primitive or cube). tmax = closest so far; a hit with t == closest is
 // accepted, so later candidates win ties exactly like hittable.rs:110-116.
@@ -441,7 +442,7 @@ RT_DEV bool leaf_hit(const DevScene& S, uint32_t code, const Ray& r, const RayD&
         }
         return false;
     }
-    if (type == rtdev::kLeafRect) {
+    if ((kF & kFLeafRM) && type == rtdev::kLeafRect) {
         if (rect_t(ld4(S.rect + 2 * idx), ld4(S.rect + 2 * idx + 1), r, tmin, closest, t)) {
             closest = t;
             hit_code = code;
@@ -476,7 +477,7 @@ RT_DEV bool leaf_hit(const DevScene& S, uint32_t code, const Ray& r, const RayD&
         }
         return false;
     }
-    if (type == rtdev::kLeafMSphere) {
+    if ((kF & kFLeafRM) && type == rtdev::kLeafMSphere) {
         if (msphere_t(ld4(S.msph + 3 * idx), ld4(S.msph + 3 * idx + 1), ld4(S.msph + 3 * idx + 2), r, tmin, closest,
                       t)) {
             closest = t;
@@ -1176,8 +1177,8 @@ RT_DEV bool entry_geom_hit(const DevScene& S, float delta, const DevEntry* E, Ra
     }
     RayD q = to_d(r);
     ABLATE(kAbGeom2, float c2 = closest; uint32_t h2 = 0u;
-           if (leaf_hit<kF>(S, E->payload, r, q, tmin, c2, h2) && h2 == 0x7fffffffu) closest = -1.0f;);
-    return leaf_hit<kF>(S, E->payload, r, q, tmin, closest, hit_code);
+           if (leaf_hit<kF | kFLeafRM>(S, E->payload, r, q, tmin, c2, h2) && h2 == 0x7fffffffu) closest = -1.0f;);
+    return leaf_hit<kF | kFLeafRM>(S, E->payload, r, q, tmin, closest, hit_code);  // top level: any primitive
 }
 
 // ConstantMedium::hit (hittable.rs:176-233); draws one U(0,1) once the clamped
@@ -2091,7 +2092,7 @@ int rt_scene_upload(const rt_scene_desc* desc, int device, rt_scene_handle* out)
     d.hrpp_nkeys = (uint32_t)hs.hrpp_keys.size();
     d.hrpp_npred = hs.num_predictors;
     s->coord_bound = hs.coord_bound;
-    s->features = hs.tri.empty() ? 0u : kFTri;
+    s->features = (hs.tri.empty() ? 0u : kFTri) | (hs.bvh_rect_msph ? kFLeafRM : 0u);
 #ifndef RT_LEAF_AUDIT  // (the audit build replays traversals on the same LDS stack: no spill area)
     {  // deep BVHs: the LDS stack keeps kStackLdsMax entries, HBM the rest
         uint32_t cap = kStackLdsMax;

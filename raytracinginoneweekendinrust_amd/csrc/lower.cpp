@@ -541,6 +541,9 @@ class Lowerer {
                                                     std::to_string(ni) + " kind " + std::to_string(c.kind) + ")");
             if ((rc = lower_prim(ni, &items[i].code))) return rc;
             if (c.kind == RT_OBJ_MOVING_SPHERE || c.kind == RT_OBJ_TRI) prunable = false;
+            if (c.kind == RT_OBJ_MOVING_SPHERE || c.kind == RT_OBJ_XY_RECT || c.kind == RT_OBJ_XZ_RECT ||
+                c.kind == RT_OBJ_YZ_RECT)
+                s_->bvh_rect_msph = true;
             items[i].box01 = prim_box(c, n.f[0], n.f[1]);
             Box b00 = prim_box(c, 0.0f, 0.0f);  // box_compare uses bounding_box(0.0, 0.0), bvh.rs:421-422
             items[i].key[0] = b00.mn.x;

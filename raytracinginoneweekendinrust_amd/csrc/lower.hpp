@@ -22,6 +22,7 @@ struct HostScene {
     std::vector<rtdev::DevTexture> texs;
     std::vector<uint8_t> perm, texels;
     uint32_t max_bvh_depth = 0;  // internal levels of the deepest BVH (reference BVH2)
+    bool bvh_rect_msph = false;  // some BVH has rect or moving-sphere leaves (the fast kernel's kFLeafRM)
     uint32_t max_stack = 1;      // BVH4 traversal stack entries (2 words) per lane
     uint32_t max_stack_ref = 1;  // the same for the BVH2 replay (reference kernel)
     // Upper bound on |coordinate| of any primitive in any instance frame plus the
