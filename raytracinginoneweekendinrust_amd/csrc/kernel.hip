@@ -64,7 +64,7 @@ enum ProfRegion : uint32_t {
 // traversal mode bits (bvh_hit): kModeExact = RT_FLAG_EXACT_BVH; the rest come
 // from DevParams::tune (RT_TUNE environment variable, diagnostics / A-B runs).
 constexpr uint32_t kModeExact = 1u, kModeNoLeafBoxes = 2u, kModeNoPermLds = 32u, kModeW3 = 64u,
-                   kModeNoPretest = 128u;
+                   kModeNoPretest = 128u, kModeReplayRef = 1u << 16;  // ReplayRef: the replay pass runs trace_samples<1>
 #ifdef RT_ABLATE
 // Ablation build (librtamd_ablate.so, diagnostics only): RT_TUNE bits that run a
 // piece of work twice (results of the copy discarded through an opaque test),
@@ -857,7 +857,9 @@ RT_DEV void sort2(float& ta, uint32_t& ca, float& tb, uint32_t& cb) {  // branch
     cb = sw ? x : y;
 }
 // kKind 0: the fast BVH4 kernel; 1: the reference kernel replays bvh.rs literally;
-// 2: the reference kernel with HRPP predictors (RT_FLAG_HRPP experiment). The fast kernel
+// 2: the reference kernel with HRPP predictors (RT_FLAG_HRPP experiment); 3: the replay
+// pass, fast traversal for every ray the fast kernel can take and the literal replay for
+// the others, so a handed-over sample's other bounces run at fast speed. The fast kernel
 // returns with `replay` set for a ray that could take a NaN hit: a ray parallel
 // to an axis plane (a zero direction component) gets t = (k - o) / d = 0 / 0 from
 // a rect whose plane holds its origin, and every comparison against NaN passes
@@ -870,7 +872,7 @@ RT_DEV bool bvh_hit(const DevScene& S, float delta, uint32_t root, const Ray& r,
     const float tmax_entry = closest;
     const f4* wrapper = S.nodes + (size_t)root * rtdev::kBvhNodeF4;
     const V inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
-    if constexpr (kKind != 0) {
+    if constexpr (kKind == 1 || kKind == 2) {
         const RayD q = to_d(r);
         const uint32_t w2 = __float_as_uint(wrapper[7].z);
         if constexpr (kKind == 2) {
@@ -886,7 +888,18 @@ RT_DEV bool bvh_hit(const DevScene& S, float delta, uint32_t root, const Ray& r,
     // empty slots' infinite boxes must never see. The reference kernel takes them.
     {
         const float ax = __builtin_fabsf(inv.x), ay = __builtin_fabsf(inv.y), az = __builtin_fabsf(inv.z);
-        if (!(ax > 0.0f && ax < kInf && ay > 0.0f && ay < kInf && az > 0.0f && az < kInf)) {
+        // A non-finite origin is handed over too: a NaN rect hit (above) leaves a NaN
+        // origin for the next bounce, which the replay pass can meet after a bounce the
+        // fast kernel never traced.
+        const bool fast = ax > 0.0f && ax < kInf && ay > 0.0f && ay < kInf && az > 0.0f && az < kInf &&
+                          __builtin_fabsf(r.o.x) < kInf && __builtin_fabsf(r.o.y) < kInf &&
+                          __builtin_fabsf(r.o.z) < kInf;
+        if constexpr (kKind == 3) {
+            if (!fast)
+                return bvh_hit_reference(S, __float_as_uint(wrapper[7].z), r, to_d(r), inv, tmin, closest, hit_code,
+                                         stk);
+        }
+        if (!fast) {
             replay = true;
             return false;
         }
@@ -1759,7 +1772,7 @@ __global__ __launch_bounds__(64, kWaves) void trace_samples(DevScene Sg, DevCame
     unsigned* counter = &ctr->batch;
     const ReplayItem* list = nullptr;
     uint32_t list_n = 0u;
-    if (kKind == 1 && fixup) {
+    if ((kKind == 1 || kKind == 3) && fixup) {
         const uint32_t n = __hip_atomic_load(&ctr->replay_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (n <= kReplayCap) {
             if (n == 0u) return;
@@ -2407,8 +2420,17 @@ int rt_render_launch(rt_scene_handle s, const rt_camera_desc* camera, const rt_r
             const TraceKernel kf = fast_instance(s->fast_waves, s->features);
             hipLaunchKernelGGL(kf, dim3(grid), dim3(64), lds, st, s->dev, cam, dp, q, s->sbuf, s->counter, s->replay,
                                0u, d_segments);
-            hipLaunchKernelGGL(trace_samples<1>, dim3(grid_ref), dim3(64), lds_ref, st, dev_ref, cam, dp, q,
-                               s->sbuf, s->counter, s->replay, 1u, d_segments);
+            if (!(s->features & kFDeep) && !(dp.tune & kModeReplayRef)) {
+                // the replay pass: fast traversal except for the rays that were handed over
+                DevScene dev_rp = s->dev;
+                dev_rp.stack_depth = std::max(s->dev.stack_depth, s->stack_ref);
+                const size_t lds_rp = (size_t)dev_rp.stack_depth * 128u * sizeof(uint32_t) + perm_lds;
+                hipLaunchKernelGGL((trace_samples<3, 3, kFAll & ~kFDeep>), dim3(grid_ref), dim3(64), lds_rp, st,
+                                   dev_rp, cam, dp, q, s->sbuf, s->counter, s->replay, 1u, d_segments);
+            } else {
+                hipLaunchKernelGGL(trace_samples<1>, dim3(grid_ref), dim3(64), lds_ref, st, dev_ref, cam, dp, q,
+                                   s->sbuf, s->counter, s->replay, 1u, d_segments);
+            }
         }
         if ((e = hipGetLastError()) != hipSuccess) return hip_fail(e, "trace_samples launch");
         if (getenv("RT_LAUNCH_LOG")) {  // diagnostics: samples the fast kernel handed to the reference kernel

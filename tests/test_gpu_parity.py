@@ -306,3 +306,23 @@ def test_stack_spill_to_hbm_matches_oracle(cfg_name, rt, orc, monkeypatch):
     got, st = gpu_render(rt, scene, cfg.camera(), params)
     np.testing.assert_array_equal(got, want)
     assert st["segments"] == cnt["segments"]
+
+
+@pytest.mark.parametrize("replay_ref", [False, True])
+@pytest.mark.parametrize("cfg_name,w,h", [("C3", 40, None), ("C5", 41, None), ("C3", 7, 1)])
+def test_replay_pass_kernels_match_oracle(cfg_name, w, h, replay_ref, rt, orc, monkeypatch):
+    # Samples the fast kernel hands over (rays with a zero / non-finite 1/d component) are
+    # re-traced by trace_samples<3> (fast traversal except for those rays), or with
+    # RT_TUNE bit 16 by the literal replay trace_samples<1>. H = 1 makes every ray such a ray.
+    if replay_ref:
+        monkeypatch.setenv("RT_TUNE", str(1 << 16))
+    cfg, scene, params = setup(rt, cfg_name, w, 3, seed=5)
+    cam = cfg.camera()
+    if h is not None:
+        cam = rt.Camera.new(cfg.look_from, cfg.look_at, cfg.view_up, cfg.vfov, w / h, cfg.aperture,
+                            cfg.focus_dist, cfg.time0, cfg.time1)
+        params = rt.render_params(w, h, 3, cfg.depth, background=cfg.background(), seed=5)
+    want, cnt = orc.render(scene, cam, params)
+    got, st = gpu_render(rt, scene, cam, params)
+    np.testing.assert_array_equal(got, want)
+    assert st["segments"] == cnt["segments"]
