@@ -2392,6 +2392,8 @@ int rt_render_launch(rt_scene_handle s, const rt_camera_desc* camera, const rt_r
         q.sample0 = p->sample_base + c * chunk;
         q.samples = c + 1 < nchunks ? chunk : p->samples_per_pixel - c * chunk;
         q.group = batch_group(q.samples);
+        if (const char* env = getenv("RT_GROUP"))  // diagnostics / A-B runs: samples per batch (1..64)
+            q.group = std::max(1u, std::min(64u, (uint32_t)strtoul(env, nullptr, 10)));
         q.groups_per_block = (q.samples + q.group - 1) / q.group;
         q.num_batches = nblk * q.groups_per_block;
         q.npix = (uint32_t)npix;
