@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 1
+#define RT_ABI_VERSION 2
 
 typedef enum rt_status {
     RT_OK = 0,
@@ -77,9 +77,34 @@ typedef enum rt_node_kind {
                                  used only under RT_FLAG_HRPP)        bvh.rs:69-80        */
     RT_OBJ_TRANSLATE = 41,    /* ref[0] child, f[0..3] displacement  instance.rs:23      */
     RT_OBJ_ROTATE_Y = 42,     /* ref[0] child, f[0] degrees          instance.rs:63      */
-    RT_OBJ_CONSTANT_MEDIUM = 43 /* ref[0] boundary, ref[1] phase albedo texture,
+    RT_OBJ_CONSTANT_MEDIUM = 43,/* ref[0] boundary, ref[1] phase albedo texture,
                                  f[0] density                        hittable.rs:150-174 */
+    RT_OBJ_BVH_TREE = 44      /* an already built Bvh (bvh.rs:38-43): its BvhNode array
+                                 as the reference holds it. ref[0] first rt_bvh_node of
+                                 the tree in rt_scene_desc.bvh_nodes, ref[1] node count,
+                                 ref[2] root_index (relative to ref[0]), f[0] time0,
+                                 f[1] time1 (unused by the hot path), f[2] = 1: built
+                                 with Bvh::with_predictor (HRPP only). The device
+                                 traverses this tree as given: its shape and boxes
+                                 decide every box test and every DFS-rank tie. */
 } rt_node_kind;
+
+/* One reference BvhNode (src/bvh.rs:228-235), children as the enum Child
+ * (bvh.rs:30-33). A node's children are both Child::Hittable (the 1-2 object
+ * leaves new_helper makes; a 1-object node repeats its object, bvh.rs:261-264)
+ * or both Child::Index. */
+#define RT_BVH_LEFT_HITTABLE 1u   /* left is Child::Hittable(IR node index)       */
+#define RT_BVH_RIGHT_HITTABLE 2u  /* right is Child::Hittable(IR node index)      */
+typedef struct rt_bvh_node {
+    int32_t left, right;   /* Child::Index(i): node i of the same tree (relative
+                              to the tree's first node); Child::Hittable: the IR
+                              node index of the object (a primitive / Cube)     */
+    uint32_t flags;        /* RT_BVH_*_HITTABLE                                 */
+    int32_t parent;        /* Option<usize> parent, -1 = None (not needed by the
+                              exact traversal; kept so the array mirrors BvhNode) */
+    float bbox_min[3];     /* bounding_box: tested as given, like bvh.rs:370    */
+    float bbox_max[3];
+} rt_bvh_node;             /* 40 bytes */
 
 typedef struct rt_node {
     uint32_t kind;   /* rt_node_kind */
@@ -97,10 +122,13 @@ typedef struct rt_scene_desc {
     uint32_t reserved0;
     const uint8_t* image_data;  /* RGB8 texels of every RT_TEX_IMAGE */
     uint64_t image_bytes;
+    const rt_bvh_node* bvh_nodes; /* node arrays of every RT_OBJ_BVH_TREE (may be NULL) */
+    uint32_t num_bvh_nodes;
+    uint32_t reserved1;
 } rt_scene_desc;
 
 /* Raw arguments of Camera::new (src/camera.rs:44-81); the basis is derived
- * on the host exactly as the reference does. */
+ * on the host exactly as the reference does (rt_camera_new). */
 typedef struct rt_camera_desc {
     float look_from[3];
     float look_at[3];
@@ -112,6 +140,21 @@ typedef struct rt_camera_desc {
     float time0;
     float time1;
 } rt_camera_desc;
+
+/* A constructed Camera: exactly the nine fields the reference's Camera stores
+ * (src/camera.rs:6-27), which is all Renderer::render receives
+ * (src/renderer.rs:42-52). Camera::get_ray (camera.rs:96-106) reads nothing else. */
+typedef struct rt_camera {
+    float origin[3];
+    float horizontal[3];
+    float vertical[3];
+    float lower_left_corner[3];
+    float u[3];
+    float v[3];
+    float lens_radius;
+    float time_start;
+    float time_end;
+} rt_camera;
 
 #define RT_FLAG_EXACT_BVH 1u  /* box tests use the BVH entry t_max like bvh.rs:363-417
                                  (no closest-hit pruning); results are identical
@@ -178,7 +221,11 @@ int rt_scene_info(rt_scene_handle scene, uint64_t counts[10]);
 
 /* Asynchronous render on `stream` (hipStream_t, NULL = default stream) into a
  * DEVICE buffer of W*H*3 floats; only the shard's pixels are written.
- * d_segments (device uint64, may be NULL) is incremented by the segments traced. */
+ * d_segments (device uint64, may be NULL) is incremented by the segments traced.
+ * Renders on one scene handle are serialised: a launch waits (on the device,
+ * hipStreamWaitEvent) for the previous launch on the same handle to finish,
+ * whatever stream either was issued on, because they share the handle's sample
+ * buffer and counters; concurrent calls from several threads are safe. */
 int rt_render_launch(rt_scene_handle scene, const rt_camera_desc* camera,
                      const rt_render_params* params, float* d_out,
                      unsigned long long* d_segments, void* stream);
@@ -230,6 +277,42 @@ int rt_scene_trace_time(rt_scene_handle scene, double* total_ms, uint64_t* launc
  * HOST buffer of W*H*3 floats (pixels outside the shard are left untouched). */
 int rt_render(rt_scene_handle scene, const rt_camera_desc* camera,
               const rt_render_params* params, float* host_out, rt_stats* stats);
+
+/* Camera::new (src/camera.rs:44-81) on the host: the nine fields the reference's
+ * Camera stores. RT_ERR_INVALID when time0 > time1 (the reference panics in
+ * Uniform::new_inclusive at the first get_ray). */
+int rt_camera_new(const rt_camera_desc* args, rt_camera* out);
+
+/* rt_render / rt_render_launch / rt_render_multi for a constructed Camera:
+ * the exact arguments of Renderer::render (src/renderer.rs:42-52), which
+ * borrows a built `Camera`, not its constructor arguments. The desc forms above
+ * are rt_camera_new followed by these. Same results bit for bit. */
+int rt_render_camera(rt_scene_handle scene, const rt_camera* camera,
+                     const rt_render_params* params, float* host_out, rt_stats* stats);
+int rt_render_launch_camera(rt_scene_handle scene, const rt_camera* camera,
+                            const rt_render_params* params, float* d_out,
+                            unsigned long long* d_segments, void* stream);
+int rt_render_multi_camera(rt_scene_handle* scenes, uint32_t n, const rt_camera* camera,
+                           const rt_render_params* params, float* host_out, rt_stats* stats);
+
+/* Multi-process frame assembly (one process per GPU, no
+ * collective). Rank r of n renders the 8x8 blocks b with b % n == r into a
+ * full-frame device image (shard_index = r, shard_count = n);
+ * rt_shard_pack copies those blocks, in block order, 64 pixel slots per block
+ * (row-major in the block; slots outside the image of an edge block are left
+ * unwritten), into a device buffer of rt_shard_floats(W, H, r, n) floats, which
+ * the rank copies (hipMemcpyAsync) into its slot of a shared buffer at float
+ * offset rt_shard_offset(W, H, r, n); rt_shard_offset(W, H, n, n) is the total.
+ * rt_shard_unpack scatters all n packed shards (one device buffer, shard r at
+ * its offset) back into a W*H*3 image. Both are asynchronous on `stream`.
+ * Packing then unpacking every rank's shard reproduces the one-device image bit
+ * for bit (pure copies). Returns 0 from the two size functions for n == 0. */
+uint64_t rt_shard_floats(uint32_t width, uint32_t height, uint32_t rank, uint32_t n);
+uint64_t rt_shard_offset(uint32_t width, uint32_t height, uint32_t rank, uint32_t n);
+int rt_shard_pack(const float* d_image, uint32_t width, uint32_t height, uint32_t rank,
+                  uint32_t n, float* d_packed, void* stream);
+int rt_shard_unpack(const float* d_packed_all, uint32_t width, uint32_t height,
+                    uint32_t n, float* d_image, void* stream);
 
 /* Scene builders restated from src/main.rs:185-829 ("random-spheres",
  * "random-moving-spheres", "two-spheres", "marble", "earth", "simple-lights",

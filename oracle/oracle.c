@@ -571,6 +571,7 @@ static int hittable_bbox(const OHit* h, float t0, float t1, OAabb* out) {
             return 1;
         }
         case RT_OBJ_BVH: /* bvh.rs:102-104 */
+        case RT_OBJ_BVH_TREE:
             return bvh_bbox(&h->bvh, out);
         case RT_OBJ_TRANSLATE: { /* instance.rs:45-52 */
             OAabb b;
@@ -739,7 +740,7 @@ static int get_hit(OScene* s, int idx, const OHit** out) {
     int rc = build_node(s, idx, &p);
     if (rc) return rc;
     uint32_t k = s->d->nodes[idx].kind;
-    if (k < RT_OBJ_SPHERE || k > RT_OBJ_CONSTANT_MEDIUM) return fail(RT_ERR_INVALID, "node %d is not a hittable", idx);
+    if (k < RT_OBJ_SPHERE || k > RT_OBJ_BVH_TREE) return fail(RT_ERR_INVALID, "node %d is not a hittable", idx);
     *out = (const OHit*)p;
     return 0;
 }
@@ -825,7 +826,7 @@ static int build_node(OScene* s, int idx, void** out) {
         default:
             break;
     }
-    if (n->kind < RT_OBJ_SPHERE || n->kind > RT_OBJ_CONSTANT_MEDIUM)
+    if (n->kind < RT_OBJ_SPHERE || n->kind > RT_OBJ_BVH_TREE)
         return fail(RT_ERR_INVALID, "node %d: unknown kind %u", idx, n->kind);
     OHit* h = (OHit*)arena_alloc(s, sizeof(OHit));
     if (!h) return fail(RT_ERR_OOM, "oom");
@@ -894,6 +895,38 @@ static int build_node(OScene* s, int idx, void** out) {
             h->bvh.root = bvh_new_helper(&h->bvh, objs, objs + cnt, cnt, n->f[0], n->f[1], &ar, &err);
             free(objs);
             if (err) return fail(RT_ERR_INVALID, "Missing bounding box in BVH construction");
+            break;
+        }
+        case RT_OBJ_BVH_TREE: { /* an already built Bvh (bvh.rs:38-43): BvhNode array as given */
+            const rt_bvh_node* bn = s->d->bvh_nodes;
+            if (n->ref[0] < 0 || n->ref[1] <= 0 || !bn ||
+                (uint64_t)n->ref[0] + (uint64_t)n->ref[1] > s->d->num_bvh_nodes)
+                return fail(RT_ERR_INVALID, "BVH tree %d: node range out of bounds", idx);
+            if (n->ref[2] < 0 || n->ref[2] >= n->ref[1]) return fail(RT_ERR_INVALID, "BVH tree %d: bad root", idx);
+            int cnt = n->ref[1];
+            h->bvh.cap = h->bvh.n = cnt;
+            h->bvh.root = n->ref[2];
+            h->bvh.nodes = (OBvhNode*)arena_alloc(s, sizeof(OBvhNode) * (size_t)cnt);
+            if (!h->bvh.nodes) return fail(RT_ERR_OOM, "oom");
+            for (int i = 0; i < cnt; ++i) {
+                const rt_bvh_node* b = &bn[n->ref[0] + i];
+                OBvhNode* nd = &h->bvh.nodes[i];
+                OChild* ch[2] = {&nd->left, &nd->right};
+                int32_t ref[2] = {b->left, b->right};
+                uint32_t hit_flag[2] = {RT_BVH_LEFT_HITTABLE, RT_BVH_RIGHT_HITTABLE};
+                for (int k = 0; k < 2; ++k) {
+                    memset(ch[k], 0, sizeof *ch[k]);
+                    if (b->flags & hit_flag[k]) { /* Child::Hittable */
+                        if ((rc = get_hit(s, ref[k], &ch[k]->obj))) return rc;
+                    } else { /* Child::Index */
+                        if (ref[k] < 0 || ref[k] >= cnt) return fail(RT_ERR_INVALID, "BVH tree %d: child out of range", idx);
+                        ch[k]->is_index = 1;
+                        ch[k]->idx = ref[k];
+                    }
+                }
+                nd->box.mn = v3(b->bbox_min[0], b->bbox_min[1], b->bbox_min[2]);
+                nd->box.mx = v3(b->bbox_max[0], b->bbox_max[1], b->bbox_max[2]);
+            }
             break;
         }
         case RT_OBJ_TRANSLATE:
@@ -1142,7 +1175,8 @@ static int hittable_hit(const OHit* h, const ORay* r, float tmin, float tmax, OC
         case RT_OBJ_TRI: return tri_hit(h, r, tmin, tmax, c, rec);
         case RT_OBJ_CUBE: /* cube.rs:84-93 */
         case RT_OBJ_LIST: return list_hit(h->items, h->nitems, r, tmin, tmax, c, rec);
-        case RT_OBJ_BVH: return bvh_node_hit(&h->bvh, h->bvh.root, r, tmin, tmax, c, rec);
+        case RT_OBJ_BVH:
+        case RT_OBJ_BVH_TREE: return bvh_node_hit(&h->bvh, h->bvh.root, r, tmin, tmax, c, rec);
         case RT_OBJ_TRANSLATE: { /* instance.rs:32-43 */
             ORay off = {vsub(r->o, h->disp), r->d, r->time};
             if (!hittable_hit(h->child, &off, tmin, tmax, c, rec)) return 0;
@@ -1333,6 +1367,20 @@ static int camera_new(const rt_camera_desc* d, uint32_t flags, OCam* cam) {
         return fail(RT_ERR_INVALID, "Uniform::new_inclusive called with `low > high`");
     return 0;
 }
+/* A constructed Camera (src/camera.rs:6-27) as Renderer::render receives it. */
+static int camera_from_fields(const rt_camera* k, OCam* cam) {
+    cam->origin = v3(k->origin[0], k->origin[1], k->origin[2]);
+    cam->horizontal = v3(k->horizontal[0], k->horizontal[1], k->horizontal[2]);
+    cam->vertical = v3(k->vertical[0], k->vertical[1], k->vertical[2]);
+    cam->llc = v3(k->lower_left_corner[0], k->lower_left_corner[1], k->lower_left_corner[2]);
+    cam->u = v3(k->u[0], k->u[1], k->u[2]);
+    cam->v = v3(k->v[0], k->v[1], k->v[2]);
+    cam->lens_radius = k->lens_radius;
+    cam->time_low = k->time_start;
+    if (!uniform_inclusive(k->time_start, k->time_end, &cam->time_scale))
+        return fail(RT_ERR_INVALID, "Uniform::new_inclusive called with `low > high`");
+    return 0;
+}
 void oracle_camera_basis(const rt_camera_desc* d, float out[21]) {
     OCam c;
     memset(&c, 0, sizeof c);
@@ -1461,11 +1509,11 @@ static int check_params(const rt_render_params* p) {
     return 0;
 }
 
-int oracle_render(const rt_scene_desc* scene, const rt_camera_desc* camera, const rt_render_params* p,
-                  const oracle_options* opt, float* out, oracle_counters* counters) {
+static int render_with(const rt_scene_desc* scene, const rt_camera_desc* camera, const rt_camera* fields,
+                       const rt_render_params* p, const oracle_options* opt, float* out, oracle_counters* counters) {
     int rc = check_params(p);
     if (rc) return rc;
-    if (!camera || !out) return fail(RT_ERR_INVALID, "camera/out is NULL");
+    if ((!camera && !fields) || !out) return fail(RT_ERR_INVALID, "camera/out is NULL");
     uint32_t flags = opt ? opt->flags : 0u;
     OScene s;
     if ((rc = scene_build(&s, scene, flags))) {
@@ -1473,7 +1521,7 @@ int oracle_render(const rt_scene_desc* scene, const rt_camera_desc* camera, cons
         return rc;
     }
     OCam cam;
-    if ((rc = camera_new(camera, flags, &cam))) {
+    if ((rc = camera ? camera_new(camera, flags, &cam) : camera_from_fields(fields, &cam))) {
         scene_free(&s);
         return rc;
     }
@@ -1518,6 +1566,17 @@ int oracle_render(const rt_scene_desc* scene, const rt_camera_desc* camera, cons
         counters->threads = started + 1;
     }
     return 0;
+}
+
+int oracle_render(const rt_scene_desc* scene, const rt_camera_desc* camera, const rt_render_params* p,
+                  const oracle_options* opt, float* out, oracle_counters* counters) {
+    return render_with(scene, camera, NULL, p, opt, out, counters);
+}
+
+int oracle_render_camera(const rt_scene_desc* scene, const rt_camera* camera, const rt_render_params* p,
+                         const oracle_options* opt, float* out, oracle_counters* counters) {
+    if (!camera) return fail(RT_ERR_INVALID, "camera is NULL");
+    return render_with(scene, NULL, camera, p, opt, out, counters);
 }
 
 int oracle_sample(const rt_scene_desc* scene, const rt_camera_desc* camera, const rt_render_params* p,

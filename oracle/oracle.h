@@ -66,6 +66,12 @@ int oracle_render(const rt_scene_desc* scene, const rt_camera_desc* camera,
                   const rt_render_params* params, const oracle_options* options,
                   float* out, oracle_counters* counters);
 
+/* oracle_render for a constructed Camera (src/camera.rs:6-27), as Renderer::render
+ * receives it. */
+int oracle_render_camera(const rt_scene_desc* scene, const rt_camera* camera,
+                         const rt_render_params* params, const oracle_options* options,
+                         float* out, oracle_counters* counters);
+
 /* Radiance of one camera sample (forward or recursive per flags). */
 int oracle_sample(const rt_scene_desc* scene, const rt_camera_desc* camera,
                   const rt_render_params* params, uint32_t flags, uint32_t x,

@@ -47,6 +47,9 @@ def _load() -> C.CDLL:
     lib.oracle_render.restype = C.c_int
     lib.oracle_render.argtypes = [P(_capi.rt_scene_desc), P(_capi.rt_camera_desc), P(_capi.rt_render_params),
                                   P(oracle_options), P(C.c_float), P(oracle_counters)]
+    lib.oracle_render_camera.restype = C.c_int
+    lib.oracle_render_camera.argtypes = [P(_capi.rt_scene_desc), P(_capi.rt_camera), P(_capi.rt_render_params),
+                                         P(oracle_options), P(C.c_float), P(oracle_counters)]
     lib.oracle_sample.restype = C.c_int
     lib.oracle_sample.argtypes = [P(_capi.rt_scene_desc), P(_capi.rt_camera_desc), P(_capi.rt_render_params),
                                   C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, P(C.c_float)]
@@ -82,9 +85,14 @@ def render(scene, camera, params, *, flags: int = 0, threads: int = 0, out: np.n
         out = np.zeros((params.height, params.width, 3), dtype=np.float32)
     opt = oracle_options(flags, threads)
     cnt = oracle_counters()
-    cam = camera.desc()
-    _check(lib.oracle_render(scene.desc, C.byref(cam), C.byref(params), C.byref(opt),
-                             out.ctypes.data_as(C.POINTER(C.c_float)), C.byref(cnt)), "oracle_render")
+    if hasattr(camera, "fields"):  # a constructed Camera (CameraBasis)
+        cam = camera.fields()
+        _check(lib.oracle_render_camera(scene.desc, C.byref(cam), C.byref(params), C.byref(opt),
+                                        out.ctypes.data_as(C.POINTER(C.c_float)), C.byref(cnt)), "oracle_render_camera")
+    else:
+        cam = camera.desc()
+        _check(lib.oracle_render(scene.desc, C.byref(cam), C.byref(params), C.byref(opt),
+                                 out.ctypes.data_as(C.POINTER(C.c_float)), C.byref(cnt)), "oracle_render")
     return out, cnt.as_dict()
 
 

@@ -18,7 +18,9 @@ ASSET_DIR = os.path.normpath(os.path.join(_HERE, "..", "assets"))
 RT_TEX_SOLID, RT_TEX_CHECKER, RT_TEX_MARBLE, RT_TEX_IMAGE = 1, 2, 3, 4
 RT_MAT_LAMBERTIAN, RT_MAT_METAL, RT_MAT_DIELECTRIC, RT_MAT_DIFFUSE_LIGHT, RT_MAT_ISOTROPIC = 16, 17, 18, 19, 20
 (RT_OBJ_SPHERE, RT_OBJ_MOVING_SPHERE, RT_OBJ_XY_RECT, RT_OBJ_XZ_RECT, RT_OBJ_YZ_RECT, RT_OBJ_CUBE, RT_OBJ_TRI,
- RT_OBJ_LIST, RT_OBJ_BVH, RT_OBJ_TRANSLATE, RT_OBJ_ROTATE_Y, RT_OBJ_CONSTANT_MEDIUM) = range(32, 44)
+ RT_OBJ_LIST, RT_OBJ_BVH, RT_OBJ_TRANSLATE, RT_OBJ_ROTATE_Y, RT_OBJ_CONSTANT_MEDIUM, RT_OBJ_BVH_TREE) = range(32, 45)
+RT_BVH_LEFT_HITTABLE, RT_BVH_RIGHT_HITTABLE = 1, 2
+ABI_VERSION = 2
 
 RT_FLAG_EXACT_BVH = 1
 RT_FLAG_HRPP = 2
@@ -33,16 +35,29 @@ class rt_node(C.Structure):
     _fields_ = [("kind", C.c_uint32), ("ref", C.c_int32 * 3), ("f", C.c_float * 12), ("seed", C.c_uint64)]
 
 
+class rt_bvh_node(C.Structure):
+    _fields_ = [("left", C.c_int32), ("right", C.c_int32), ("flags", C.c_uint32), ("parent", C.c_int32),
+                ("bbox_min", C.c_float * 3), ("bbox_max", C.c_float * 3)]
+
+
 class rt_scene_desc(C.Structure):
     _fields_ = [("nodes", C.POINTER(rt_node)), ("num_nodes", C.c_uint32), ("world", C.c_int32),
                 ("list_items", C.POINTER(C.c_int32)), ("num_list_items", C.c_uint32), ("reserved0", C.c_uint32),
-                ("image_data", C.POINTER(C.c_uint8)), ("image_bytes", C.c_uint64)]
+                ("image_data", C.POINTER(C.c_uint8)), ("image_bytes", C.c_uint64),
+                ("bvh_nodes", C.POINTER(rt_bvh_node)), ("num_bvh_nodes", C.c_uint32), ("reserved1", C.c_uint32)]
 
 
 class rt_camera_desc(C.Structure):
     _fields_ = [("look_from", C.c_float * 3), ("look_at", C.c_float * 3), ("view_up", C.c_float * 3),
                 ("vfov_deg", C.c_float), ("aspect_ratio", C.c_float), ("aperture", C.c_float),
                 ("focus_dist", C.c_float), ("time0", C.c_float), ("time1", C.c_float)]
+
+
+class rt_camera(C.Structure):
+    """The nine fields of the reference's Camera (src/camera.rs:6-27)."""
+    _fields_ = [("origin", C.c_float * 3), ("horizontal", C.c_float * 3), ("vertical", C.c_float * 3),
+                ("lower_left_corner", C.c_float * 3), ("u", C.c_float * 3), ("v", C.c_float * 3),
+                ("lens_radius", C.c_float), ("time_start", C.c_float), ("time_end", C.c_float)]
 
 
 class rt_render_params(C.Structure):
@@ -63,6 +78,9 @@ class rt_tile(C.Structure):
 
 assert C.sizeof(rt_node) == 72
 assert C.sizeof(rt_render_params) == 64
+assert C.sizeof(rt_bvh_node) == 40
+assert C.sizeof(rt_scene_desc) == 64
+assert C.sizeof(rt_camera) == 84
 
 # (name, restype, argtypes) for every symbol declared in include/rt.h
 SIGNATURES = [
@@ -91,6 +109,17 @@ SIGNATURES = [
     ("rt_bvh_build_order", C.c_int, [C.c_void_p, C.c_uint32, C.c_uint64, C.c_void_p, C.c_void_p]),
     ("rt_device_numeric_eval", C.c_int, [C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double),
                                          C.POINTER(C.c_double), C.c_uint32]),
+    ("rt_camera_new", C.c_int, [C.POINTER(rt_camera_desc), C.POINTER(rt_camera)]),
+    ("rt_render_camera", C.c_int, [C.c_void_p, C.POINTER(rt_camera), C.POINTER(rt_render_params),
+                                   C.POINTER(C.c_float), C.POINTER(rt_stats)]),
+    ("rt_render_launch_camera", C.c_int, [C.c_void_p, C.POINTER(rt_camera), C.POINTER(rt_render_params), C.c_void_p,
+                                          C.c_void_p, C.c_void_p]),
+    ("rt_render_multi_camera", C.c_int, [C.POINTER(C.c_void_p), C.c_uint32, C.POINTER(rt_camera),
+                                         C.POINTER(rt_render_params), C.POINTER(C.c_float), C.POINTER(rt_stats)]),
+    ("rt_shard_floats", C.c_uint64, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]),
+    ("rt_shard_offset", C.c_uint64, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]),
+    ("rt_shard_pack", C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p]),
+    ("rt_shard_unpack", C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p]),
 ]
 
 
@@ -112,7 +141,7 @@ def load() -> C.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.rt_abi_version() != 1:
+    if lib.rt_abi_version() != ABI_VERSION:
         raise ImportError("librtamd.so ABI version mismatch")
     return lib
 

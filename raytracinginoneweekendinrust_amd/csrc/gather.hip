@@ -1,0 +1,124 @@
+// gather.hip — frame assembly for one process per GPU.
+//
+// The reference composites its tiles into one image on the host
+// (src/renderer.rs:63-95). Here rank r of n renders the 8x8 blocks b with
+// b % n == r (rt_render_params.shard_index / shard_count, the block interleave
+// the trace kernel uses) into a full-frame device image; rt_shard_pack moves
+// those blocks into a dense buffer (64 pixel slots per block, blocks in order),
+// the rank copies it with one hipMemcpyAsync into its slot of a buffer shared
+// with rank 0, and rank 0 scatters all n shards back with rt_shard_unpack.
+// Pure copies: the assembled image is the one-device image bit for bit. Both
+// kernels are HBM-bound (12 B read + 12 B written per pixel).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+
+#include "../../include/rt.h"
+#include "common.hpp"
+
+namespace {
+
+struct Grid {
+    uint32_t bx, nb;  // blocks per row, blocks in the frame
+};
+Grid grid_of(uint32_t w, uint32_t h) { return Grid{(w + 7u) / 8u, ((w + 7u) / 8u) * ((h + 7u) / 8u)}; }
+
+// blocks of rank r: b = r, r + n, ... < nb
+__host__ __device__ inline uint64_t blocks_of(uint32_t nb, uint32_t r, uint32_t n) {
+    return r < nb ? (uint64_t)(nb - r + n - 1u) / n : 0u;
+}
+// blocks of ranks 0..r-1: r * floor(nb / n) + min(r, nb % n)
+__host__ __device__ inline uint64_t blocks_before(uint32_t nb, uint32_t r, uint32_t n) {
+    const uint32_t q = nb / n, m = nb % n;
+    return (uint64_t)r * q + (r < m ? r : m);
+}
+
+// thread = (k-th block of the rank, pixel slot p): packed[(k * 64 + p) * 3 + c]
+__global__ __launch_bounds__(256) void shard_pack(const float* __restrict__ img, uint32_t w, uint32_t h, uint32_t bx,
+                                                  uint32_t r, uint32_t n, uint64_t slots, float* __restrict__ packed) {
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < slots; i += (uint64_t)gridDim.x * 256u) {
+        const uint64_t k = i >> 6;
+        const uint32_t p = (uint32_t)(i & 63u);
+        const uint64_t b = r + k * n;
+        const uint32_t x = (uint32_t)(b % bx) * 8u + (p & 7u), y = (uint32_t)(b / bx) * 8u + (p >> 3);
+        if (x >= w || y >= h) continue;
+        const float* src = img + ((uint64_t)y * w + x) * 3u;
+        float* dst = packed + i * 3u;
+        dst[0] = src[0];
+        dst[1] = src[1];
+        dst[2] = src[2];
+    }
+}
+
+// thread = (frame block b, pixel slot p); shard b % n holds it at slot b / n
+__global__ __launch_bounds__(256) void shard_unpack(const float* __restrict__ packed, uint32_t w, uint32_t h,
+                                                    uint32_t bx, uint32_t nb, uint32_t n, float* __restrict__ img) {
+    const uint64_t slots = (uint64_t)nb * 64u;
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < slots; i += (uint64_t)gridDim.x * 256u) {
+        const uint32_t b = (uint32_t)(i >> 6), p = (uint32_t)(i & 63u);
+        const uint32_t x = (b % bx) * 8u + (p & 7u), y = (b / bx) * 8u + (p >> 3);
+        if (x >= w || y >= h) continue;
+        const uint32_t r = b % n;
+        const uint64_t slot = (blocks_before(nb, r, n) + b / n) * 64u + p;
+        const float* src = packed + slot * 3u;
+        float* dst = img + ((uint64_t)y * w + x) * 3u;
+        dst[0] = src[0];
+        dst[1] = src[1];
+        dst[2] = src[2];
+    }
+}
+
+uint32_t launch_blocks(uint64_t work) {
+    const uint64_t b = (work + 255u) / 256u;
+    return (uint32_t)(b < 8192u ? (b ? b : 1u) : 8192u);
+}
+
+int hip_fail(hipError_t e, const char* what) {
+    return rthost::set_error(RT_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+}  // namespace
+
+extern "C" {
+
+uint64_t rt_shard_floats(uint32_t width, uint32_t height, uint32_t rank, uint32_t n) {
+    if (n == 0) return 0;
+    return blocks_of(grid_of(width, height).nb, rank, n) * 64u * 3u;
+}
+
+uint64_t rt_shard_offset(uint32_t width, uint32_t height, uint32_t rank, uint32_t n) {
+    if (n == 0) return 0;
+    const uint32_t r = rank < n ? rank : n;
+    return blocks_before(grid_of(width, height).nb, r, n) * 64u * 3u;
+}
+
+int rt_shard_pack(const float* d_image, uint32_t width, uint32_t height, uint32_t rank, uint32_t n, float* d_packed,
+                  void* stream) {
+    rthost::clear_error();
+    if (!d_image || !d_packed || n == 0 || rank >= n || width == 0 || height == 0)
+        return rthost::set_error(RT_ERR_INVALID, "rt_shard_pack: NULL buffer, empty image or rank >= n");
+    const Grid g = grid_of(width, height);
+    const uint64_t slots = blocks_of(g.nb, rank, n) * 64u;
+    if (slots == 0) return RT_OK;
+    (void)hipGetLastError();
+    hipLaunchKernelGGL(shard_pack, dim3(launch_blocks(slots)), dim3(256), 0, (hipStream_t)stream, d_image, width,
+                       height, g.bx, rank, n, slots, d_packed);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? RT_OK : hip_fail(e, "shard_pack launch");
+}
+
+int rt_shard_unpack(const float* d_packed_all, uint32_t width, uint32_t height, uint32_t n, float* d_image,
+                    void* stream) {
+    rthost::clear_error();
+    if (!d_packed_all || !d_image || n == 0 || width == 0 || height == 0)
+        return rthost::set_error(RT_ERR_INVALID, "rt_shard_unpack: NULL buffer, empty image or n == 0");
+    const Grid g = grid_of(width, height);
+    (void)hipGetLastError();
+    hipLaunchKernelGGL(shard_unpack, dim3(launch_blocks((uint64_t)g.nb * 64u)), dim3(256), 0, (hipStream_t)stream,
+                       d_packed_all, width, height, g.bx, g.nb, n, d_image);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? RT_OK : hip_fail(e, "shard_unpack launch");
+}
+
+}  // extern "C"

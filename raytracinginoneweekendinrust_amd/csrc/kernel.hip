@@ -25,6 +25,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -1951,6 +1952,10 @@ struct rt_scene {
     hipEvent_t ev[kEvents][2] = {};
     int ev_count = 0;
     bool ev_overflow = false;
+    // Launches on one handle share the workspace above: the host state is guarded by
+    // `mu`, and each launch's stream waits for the previous launch's `done` event.
+    std::mutex mu;
+    hipEvent_t done = nullptr;
 };
 
 namespace {
@@ -2209,6 +2214,7 @@ int rt_scene_free(rt_scene_handle s) {
                         ta[i].fast_t, ta[i].ref_t, ta[i].fast_code, ta[i].ref_code, ta[i].root);
         }
 #endif
+        if (s->done) (void)hipEventSynchronize(s->done);  // the last launch may still use the buffers below
         if (s->pool) (void)hipFree(s->pool);
         if (s->sbuf) (void)hipFree(s->sbuf);
         if (s->counter) (void)hipFree(s->counter);
@@ -2219,6 +2225,7 @@ int rt_scene_free(rt_scene_handle s) {
         for (int i = 0; i < rt_scene::kEvents; ++i)
             for (int j = 0; j < 2; ++j)
                 if (s->ev[i][j]) (void)hipEventDestroy(s->ev[i][j]);
+        if (s->done) (void)hipEventDestroy(s->done);
     }
     delete s;
     return RT_OK;
@@ -2270,15 +2277,34 @@ int rt_scene_info(rt_scene_handle s, uint64_t counts[10]) {
     return RT_OK;
 }
 
+int rt_camera_new(const rt_camera_desc* args, rt_camera* out) {
+    rthost::clear_error();
+    if (!args || !out) return rthost::set_error(RT_ERR_INVALID, "NULL argument");
+    std::string err;
+    int rc = rthost::camera_new(args, out, &err);
+    return rc ? rthost::set_error(rc, err) : RT_OK;
+}
+
 int rt_render_launch(rt_scene_handle s, const rt_camera_desc* camera, const rt_render_params* p, float* d_out,
                      unsigned long long* d_segments, void* stream) {
+    rthost::clear_error();
+    if (!camera) return rthost::set_error(RT_ERR_INVALID, "NULL camera");
+    rt_camera cam;
+    std::string err;
+    int rc = rthost::camera_new(camera, &cam, &err);
+    if (rc) return rthost::set_error(rc, err);
+    return rt_render_launch_camera(s, &cam, p, d_out, d_segments, stream);
+}
+
+int rt_render_launch_camera(rt_scene_handle s, const rt_camera* camera, const rt_render_params* p, float* d_out,
+                            unsigned long long* d_segments, void* stream) {
     rthost::clear_error();
     if (!s || !camera || !d_out) return rthost::set_error(RT_ERR_INVALID, "NULL scene/camera/output");
     int rc = check_params(p);
     if (rc) return rc;
     DevCamera cam;
     std::string err;
-    if ((rc = rthost::camera_basis(camera, &cam, &err))) return rthost::set_error(rc, err);
+    if ((rc = rthost::camera_device(camera, &cam, &err))) return rthost::set_error(rc, err);
     DevParams dp;
     memset(&dp, 0, sizeof dp);
     dp.width = p->width;
@@ -2315,6 +2341,15 @@ int rt_render_launch(rt_scene_handle s, const rt_camera_desc* camera, const rt_r
     if (nblk == 0) return RT_OK;
     DeviceGuard g(s->device);
     if (!g.ok) return rthost::set_error(RT_ERR_HIP, "hipSetDevice failed");
+    // One render at a time per handle: host state under the lock, and on the device
+    // this launch starts after the previous one (any stream) has finished.
+    std::lock_guard<std::mutex> lock(s->mu);
+    hipError_t e;
+    if (!s->done && (e = hipEventCreateWithFlags(&s->done, hipEventDisableTiming)) != hipSuccess) {
+        s->done = nullptr;
+        return hip_fail(e, "hipEventCreate");
+    }
+    if ((e = hipStreamWaitEvent((hipStream_t)stream, s->done, 0)) != hipSuccess) return hip_fail(e, "hipStreamWaitEvent");
     // Sample buffer: chunks of whole sample ranges (the per-pixel sum stays in order).
     const uint64_t npix = (uint64_t)p->width * p->height;
     const uint64_t per_sample = npix * 3u * sizeof(float);
@@ -2325,7 +2360,6 @@ int rt_render_launch(rt_scene_handle s, const rt_camera_desc* camera, const rt_r
     uint32_t nchunks = (uint32_t)((p->samples_per_pixel + max_s - 1) / max_s);
     uint32_t chunk = (p->samples_per_pixel + nchunks - 1) / nchunks;
     uint64_t need = per_sample * chunk;
-    hipError_t e;
     if (s->sbuf_bytes < need) {
         if (s->sbuf) (void)hipFree(s->sbuf);
         s->sbuf = nullptr;
@@ -2476,11 +2510,23 @@ int rt_render_launch(rt_scene_handle s, const rt_camera_desc* camera, const rt_r
                            c + 1 == nchunks && !(p->flags & RT_FLAG_RAW_SUM) ? 1 : 0);
         if ((e = hipGetLastError()) != hipSuccess) return hip_fail(e, "resolve_samples launch");
     }
+    if ((e = hipEventRecord(s->done, st)) != hipSuccess) return hip_fail(e, "hipEventRecord");
     return RT_OK;
 }
 
 int rt_render(rt_scene_handle s, const rt_camera_desc* camera, const rt_render_params* p, float* host_out,
               rt_stats* stats) {
+    rthost::clear_error();
+    if (!camera) return rthost::set_error(RT_ERR_INVALID, "NULL camera");
+    rt_camera cam;
+    std::string err;
+    int rc = rthost::camera_new(camera, &cam, &err);
+    if (rc) return rthost::set_error(rc, err);
+    return rt_render_camera(s, &cam, p, host_out, stats);
+}
+
+int rt_render_camera(rt_scene_handle s, const rt_camera* camera, const rt_render_params* p, float* host_out,
+                     rt_stats* stats) {
     rthost::clear_error();
     if (!s || !camera || !host_out) return rthost::set_error(RT_ERR_INVALID, "NULL scene/camera/output");
     int rc = check_params(p);
@@ -2508,7 +2554,7 @@ int rt_render(rt_scene_handle s, const rt_camera_desc* camera, const rt_render_p
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
     (void)hipEventRecord(e0, st);
-    rc = rt_render_launch(s, camera, p, d_out, d_seg, st);
+    rc = rt_render_launch_camera(s, camera, p, d_out, d_seg, st);
     if (rc) { cleanup(); return rc; }
     (void)hipEventRecord(e1, st);
     unsigned long long seg = 0;
@@ -2534,6 +2580,17 @@ int rt_render(rt_scene_handle s, const rt_camera_desc* camera, const rt_render_p
 
 int rt_render_multi(rt_scene_handle* scenes, uint32_t n, const rt_camera_desc* camera, const rt_render_params* p,
                     float* host_out, rt_stats* stats) {
+    rthost::clear_error();
+    if (!camera) return rthost::set_error(RT_ERR_INVALID, "NULL camera");
+    rt_camera cam;
+    std::string err;
+    int rc = rthost::camera_new(camera, &cam, &err);
+    if (rc) return rthost::set_error(rc, err);
+    return rt_render_multi_camera(scenes, n, &cam, p, host_out, stats);
+}
+
+int rt_render_multi_camera(rt_scene_handle* scenes, uint32_t n, const rt_camera* camera, const rt_render_params* p,
+                           float* host_out, rt_stats* stats) {
     rthost::clear_error();
     if (!scenes || n == 0 || !camera || !host_out) return rthost::set_error(RT_ERR_INVALID, "NULL argument or n == 0");
     int rc = check_params(p);
@@ -2576,10 +2633,14 @@ int rt_render_multi(rt_scene_handle* scenes, uint32_t n, const rt_camera_desc* c
             cleanup();
             return rthost::set_error(RT_ERR_OOM, "hipMalloc shard image");
         }
-        if ((e = hipMemsetAsync(x.d_out, 0, floats * sizeof(float), x.st)) != hipSuccess ||
+        // RT_FLAG_ACCUMULATE continues the running sum the caller holds in host_out,
+        // exactly like rt_render (which uploads it too)
+        if (((p->flags & RT_FLAG_ACCUMULATE)
+                 ? (e = hipMemcpyAsync(x.d_out, host_out, floats * sizeof(float), hipMemcpyHostToDevice, x.st))
+                 : (e = hipMemsetAsync(x.d_out, 0, floats * sizeof(float), x.st))) != hipSuccess ||
             (e = hipMemsetAsync(x.d_seg, 0, sizeof(unsigned long long), x.st)) != hipSuccess) {
             cleanup();
-            return hip_fail(e, "memset");
+            return hip_fail(e, "shard image init");
         }
         (void)hipEventCreate(&x.e0);
         (void)hipEventCreate(&x.e1);
@@ -2587,7 +2648,7 @@ int rt_render_multi(rt_scene_handle* scenes, uint32_t n, const rt_camera_desc* c
         rt_render_params q = *p;
         q.shard_index = n > 1 ? i : 0u;
         q.shard_count = n > 1 ? n : 0u;
-        if ((rc = rt_render_launch(scenes[i], camera, &q, x.d_out, x.d_seg, x.st))) { cleanup(); return rc; }
+        if ((rc = rt_render_launch_camera(scenes[i], camera, &q, x.d_out, x.d_seg, x.st))) { cleanup(); return rc; }
         (void)hipEventRecord(x.e1, x.st);
         x.img.resize(floats);
         if ((e = hipMemcpyAsync(x.img.data(), x.d_out, floats * sizeof(float), hipMemcpyDeviceToHost, x.st)) != hipSuccess ||
@@ -2627,6 +2688,7 @@ int rt_scene_trace_time(rt_scene_handle s, double* total_ms, uint64_t* launches,
     rthost::clear_error();
     if (!s || !total_ms || !launches) return rthost::set_error(RT_ERR_INVALID, "NULL argument");
     DeviceGuard g(s->device);
+    std::lock_guard<std::mutex> lock(s->mu);
     double sum = 0.0;
     for (int i = 0; i < s->ev_count; ++i) {
         hipError_t e = hipEventSynchronize(s->ev[i][1]);

@@ -156,7 +156,7 @@ void perlin_permutation(uint32_t seed, uint8_t out[256]) {
 // ---------------------------------------------------------------------------
 // Camera::new
 // ---------------------------------------------------------------------------
-int camera_basis(const rt_camera_desc* d, rtdev::DevCamera* c, std::string* err) {
+int camera_new(const rt_camera_desc* d, rt_camera* c, std::string* err) {
     V lf{d->look_from[0], d->look_from[1], d->look_from[2]};
     V la{d->look_at[0], d->look_at[1], d->look_at[2]};
     V vup{d->view_up[0], d->view_up[1], d->view_up[2]};
@@ -178,21 +178,45 @@ int camera_basis(const rt_camera_desc* d, rtdev::DevCamera* c, std::string* err)
     put(c->origin, lf);
     put(c->horizontal, hor);
     put(c->vertical, ver);
-    put(c->llc, llc);
+    put(c->lower_left_corner, llc);
     put(c->u, u);
     put(c->v, v);
     c->lens_radius = d->aperture / 2.0f;
-    c->time_low = d->time0;
-    // UniformFloat::new_inclusive (rand 0.8.5) for gen_range(time0..=time1), camera.rs:104
+    c->time_start = d->time0;
+    c->time_end = d->time1;
     if (!(d->time0 <= d->time1)) {
         *err = "Uniform::new_inclusive called with `low > high` (cam time0 > time1)";
         return RT_ERR_INVALID;
     }
-    const float max_rand = bitsf(0x3fffffffu | 0x3f800000u) - 1.0f;  // (u32::MAX >> 9) in [1,2) - 1
-    float scale = (d->time1 - d->time0) / max_rand;
-    while (scale * max_rand + d->time0 > d->time1) scale = bitsf(fbits(scale) - 1u);
-    c->time_scale = scale;
     return RT_OK;
+}
+
+int camera_device(const rt_camera* c, rtdev::DevCamera* out, std::string* err) {
+    memcpy(out->origin, c->origin, sizeof out->origin);
+    memcpy(out->horizontal, c->horizontal, sizeof out->horizontal);
+    memcpy(out->vertical, c->vertical, sizeof out->vertical);
+    memcpy(out->llc, c->lower_left_corner, sizeof out->llc);
+    memcpy(out->u, c->u, sizeof out->u);
+    memcpy(out->v, c->v, sizeof out->v);
+    out->lens_radius = c->lens_radius;
+    out->time_low = c->time_start;
+    // UniformFloat::new_inclusive (rand 0.8.5) for gen_range(time_start..=time_end), camera.rs:104
+    if (!(c->time_start <= c->time_end)) {
+        *err = "Uniform::new_inclusive called with `low > high` (camera time_start > time_end)";
+        return RT_ERR_INVALID;
+    }
+    const float max_rand = bitsf(0x3fffffffu | 0x3f800000u) - 1.0f;  // (u32::MAX >> 9) in [1,2) - 1
+    float scale = (c->time_end - c->time_start) / max_rand;
+    while (scale * max_rand + c->time_start > c->time_end) scale = bitsf(fbits(scale) - 1u);
+    out->time_scale = scale;
+    return RT_OK;
+}
+
+int camera_basis(const rt_camera_desc* d, rtdev::DevCamera* c, std::string* err) {
+    rt_camera cam;
+    int rc = camera_new(d, &cam, err);
+    if (rc) return rc;
+    return camera_device(&cam, c, err);
 }
 
 // ---------------------------------------------------------------------------
@@ -614,6 +638,93 @@ class Lowerer {
             return (uint32_t)tn.size() - 1;
         };
         uint32_t troot = helper(items.data(), count, 1);
+        return bvh_emit(tn, troot, prunable, n.ref[1] == 1, root_out);
+    }
+
+    // RT_OBJ_BVH_TREE: a Bvh the caller has already built (bvh.rs:38-43), lowered
+    // as given: its shape, boxes and child order decide the visit set and every
+    // DFS-rank tie, exactly as BvhNode::hit (bvh.rs:363-417) walks that array.
+    int bvh_tree(const rt_node& n, uint32_t* root_out) {
+        if (n.ref[0] < 0 || n.ref[1] <= 0 || !d_->bvh_nodes ||
+            (uint64_t)n.ref[0] + (uint64_t)n.ref[1] > d_->num_bvh_nodes)
+            return fail(RT_ERR_INVALID, "BVH tree node range out of bounds");
+        const uint32_t first = (uint32_t)n.ref[0], cnt = (uint32_t)n.ref[1];
+        if (n.ref[2] < 0 || (uint32_t)n.ref[2] >= cnt) return fail(RT_ERR_INVALID, "BVH tree root_index out of range");
+        const rt_bvh_node* bn = d_->bvh_nodes + first;
+        std::vector<TNode> tn(cnt);
+        std::vector<uint8_t> seen(cnt, 0);
+        bool prunable = true;
+        const Box none{{0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f}};
+        // iterative preorder walk from the root: every node reached exactly once
+        std::vector<std::pair<uint32_t, uint32_t>> st{{(uint32_t)n.ref[2], 1u}};
+        while (!st.empty()) {
+            const uint32_t i = st.back().first, depth = st.back().second;
+            st.pop_back();
+            if (seen[i]) return fail(RT_ERR_INVALID, "BVH tree node " + std::to_string(i) + " reached twice");
+            seen[i] = 1;
+            if (depth > max_depth_) max_depth_ = depth;
+            if (depth > 4096) return fail(RT_ERR_UNSUPPORTED, "BVH tree deeper than 4096 levels");
+            const rt_bvh_node& b = bn[i];
+            TNode& t = tn[i];
+            t.box = Box{{b.bbox_min[0], b.bbox_min[1], b.bbox_min[2]}, {b.bbox_max[0], b.bbox_max[1], b.bbox_max[2]}};
+            t.leaf_box[0] = t.leaf_box[1] = none;
+            const bool lh = (b.flags & RT_BVH_LEFT_HITTABLE) != 0u, rh = (b.flags & RT_BVH_RIGHT_HITTABLE) != 0u;
+            if (lh != rh)
+                return fail(RT_ERR_UNSUPPORTED, "BVH tree node " + std::to_string(i) +
+                                                    " mixes Child::Index and Child::Hittable (new_helper never does)");
+            if (lh) {  // the 1-2 object leaves of bvh.rs:260-276
+                const int obj[2] = {b.left, b.right};
+                for (int k = 0; k < 2; ++k) {
+                    if (!valid(obj[k])) return fail(RT_ERR_INVALID, "BVH tree leaf object out of range");
+                    const rt_node& c = node(obj[k]);
+                    if (!is_prim(c.kind))
+                        return fail(RT_ERR_UNSUPPORTED, "device BVH leaves must be Sphere/MovingSphere/Rect/Cube/Tri");
+                    if (c.kind == RT_OBJ_MOVING_SPHERE || c.kind == RT_OBJ_TRI) prunable = false;
+                    if (c.kind == RT_OBJ_MOVING_SPHERE || c.kind == RT_OBJ_XY_RECT || c.kind == RT_OBJ_XZ_RECT ||
+                        c.kind == RT_OBJ_YZ_RECT)
+                        s_->bvh_rect_msph = true;
+                }
+                int rc;
+                t.is_node[0] = t.is_node[1] = false;
+                if ((rc = lower_prim(obj[0], &t.child[0]))) return rc;
+                t.leaf_box[0] = prim_box(node(obj[0]), n.f[0], n.f[1]);
+                if (obj[1] == obj[0]) {  // a 1-object node repeats its object: same result tested once
+                    t.child[1] = rtdev::kChildEmpty;
+                } else {
+                    if ((rc = lower_prim(obj[1], &t.child[1]))) return rc;
+                    t.leaf_box[1] = prim_box(node(obj[1]), n.f[0], n.f[1]);
+                }
+            } else {
+                const int ch[2] = {b.left, b.right};
+                for (int k = 0; k < 2; ++k) {
+                    if (ch[k] < 0 || (uint32_t)ch[k] >= cnt) return fail(RT_ERR_INVALID, "BVH tree child index out of range");
+                    t.child[k] = (uint32_t)ch[k];
+                    t.is_node[k] = true;
+                }
+                st.push_back({t.child[1], depth + 1});
+                st.push_back({t.child[0], depth + 1});
+            }
+        }
+        // The BVH4 collapse skips the box tests of interior nodes it merges away:
+        // exact only when every Index child's box lies inside its parent's (the
+        // reference builder's boxes are unions, bvh.rs:294-300, so this holds).
+        auto inside = [](const Box& c, const Box& p) {
+            return p.mn.x <= c.mn.x && p.mn.y <= c.mn.y && p.mn.z <= c.mn.z && c.mx.x <= p.mx.x && c.mx.y <= p.mx.y &&
+                   c.mx.z <= p.mx.z;
+        };
+        for (uint32_t i = 0; i < cnt; ++i) {
+            if (!seen[i]) return fail(RT_ERR_INVALID, "BVH tree node " + std::to_string(i) + " not reachable from the root");
+            for (int k = 0; k < 2; ++k)
+                if (tn[i].is_node[k] && !inside(tn[tn[i].child[k]].box, tn[i].box))
+                    return fail(RT_ERR_UNSUPPORTED, "BVH tree node " + std::to_string(tn[i].child[k]) +
+                                                        ": box not inside its parent's (not a union-built tree)");
+        }
+        return bvh_emit(tn, (uint32_t)n.ref[2], prunable, n.f[2] == 1.0f, root_out);
+    }
+
+    // Lays out one reference BVH2 (tn, root troot) for the device: the BVH4 the fast
+    // kernel traverses, the BVH2 the reference kernel replays, HRPP side data.
+    int bvh_emit(const std::vector<TNode>& tn, uint32_t troot, bool prunable, bool predictor, uint32_t* root_out) {
         // Leaf children carry their DFS ordinal in the reference tree ("rank",
         // cube faces rank + 0..5): the device may visit children in any order
         // and still resolves equal-t ties like the reference's recursion (later
@@ -753,7 +864,7 @@ class Lowerer {
         // its rank[3] carries the BVH's flags
         put(base, {Slot{true, wroot | 0x40000000u, tn[troot].box, 0u}}, prunable ? rtdev::kBvhPrunable : 0u);
         s_->nodes[(size_t)base * rtdev::kBvhNodeF4 + 7].z = bitsf(base2);  // wrapper rank[2]: the BVH2 wrapper
-        if (n.ref[1] == 1) {  // Bvh::with_predictor (bvh.rs:69-80): HRPP side data
+        if (predictor) {  // Bvh::with_predictor (bvh.rs:69-80): HRPP side data
             // The predictor table stores, per ray hash, "leaf nodes" (GO_UP_LEVEL = 0,
             // bvh.rs:22: the BvhNode whose child object was hit). Each gets a
             // wrapper-format record (its own box, child 0 = the node) so that
@@ -828,8 +939,9 @@ class Lowerer {
                 return lower_entry(n.ref[0], c2, out, depth + 1);
             }
             case RT_OBJ_BVH:
+            case RT_OBJ_BVH_TREE:
                 e.kind = rtdev::kEntBvh;
-                if ((rc = bvh_build(n, &e.payload))) return rc;
+                if ((rc = n.kind == RT_OBJ_BVH ? bvh_build(n, &e.payload) : bvh_tree(n, &e.payload))) return rc;
                 out->push_back(e);
                 return RT_OK;
             case RT_OBJ_CONSTANT_MEDIUM: {  // hittable.rs:150-174

@@ -64,6 +64,11 @@ int device_bvh_order(void* ctx, const float* keys, uint32_t n, uint64_t seed, ui
 
 // Camera::new (src/camera.rs:44-81); returns RT_ERR_INVALID when time0 > time1
 // (the reference panics in UniformFloat::new_inclusive).
+int camera_new(const rt_camera_desc* args, rt_camera* out, std::string* err);
+// The kernel's copy of a constructed Camera (src/camera.rs:6-27) plus the
+// UniformFloat::new_inclusive scale of gen_range(time_start..=time_end) (camera.rs:104).
+int camera_device(const rt_camera* cam, rtdev::DevCamera* out, std::string* err);
+// camera_new followed by camera_device.
 int camera_basis(const rt_camera_desc* cam, rtdev::DevCamera* out, std::string* err);
 
 // Philox4x32-10 (Random123), host copy used by the split-axis stream.

@@ -451,8 +451,20 @@ std::vector<float> synthetic_mesh(int level) {
     return out;
 }
 
-// tobj::load_obj(triangulate: true) restated for `v` / `f` records (src/main.rs:745-789):
-// polygons are fan-triangulated, indices may be negative, extra attributes ignored.
+// tobj 4.0.0 load_obj(triangulate: true) then `models[0]` (src/main.rs:745-789), restated for
+// `v` / `f` / `o` / `g` records: vertex positions are global to the file; a model ends
+// where an `o` or `g` record follows faces (tobj pushes a Model there and only when it
+// has faces), and the reference keeps only the first one; polygons are fan-triangulated
+// (v0, v[i-1], v[i]) like tobj's triangulate; indices may be negative (relative) and
+// carry /vt/vn parts, which are ignored. Not restated (parity unpinned): tobj splits a
+// model at `usemtl` only when an .mtl library defining the material was loaded, and
+// emits 1-2 vertex `f` records as points/lines; neither occurs in the reference's meshes.
+// True when the line at `i` starts a new tobj model (an `o` or `g` record).
+bool model_done(const std::string& text, size_t i) {
+    const char c = text[i];
+    return (c == 'o' || c == 'g') && i + 1 < text.size() && (text[i + 1] == ' ' || text[i + 1] == '\t');
+}
+
 int load_obj_tris(const std::string& path, std::vector<float>* out) {
     std::vector<uint8_t> bytes;
     if (!read_file(path, &bytes)) return set_error(RT_ERR_IO, "cannot read " + path);
@@ -461,7 +473,7 @@ int load_obj_tris(const std::string& path, std::vector<float>* out) {
     std::string text(bytes.begin(), bytes.end());
     std::vector<float> pos;
     size_t i = 0;
-    while (i < text.size()) {
+    while (i < text.size() && !(model_done(text, i) && !out->empty())) {
         size_t e = text.find('\n', i);
         if (e == std::string::npos) e = text.size();
         std::string line = text.substr(i, e - i);

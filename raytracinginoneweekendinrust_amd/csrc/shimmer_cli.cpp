@@ -10,7 +10,15 @@
 //
 // Extra flags (not in the reference): --seed N (the reference's thread_rng is
 // OS-seeded), --assets DIR, --device N, --devices N (one frame over devices
-// 0..N-1, rt_render_multi), --pfm FILE (linear float dump), --exact-bvh.
+// 0..N-1, rt_render_multi), --pfm FILE (linear float dump), --exact-bvh, --hrpp.
+//
+// HRPP: the reference CLI renders showcase, bunny, gargoyle and igea-hrpp with
+// hash-based ray path predictors on (Bvh::with_predictor, src/main.rs:586, 679,
+// 685, 828), i.e. with an approximate, non-deterministic traversal. This CLI
+// renders exactly by default (the bit-reproducible path); --hrpp turns on the
+// GPU HRPP experiment (RT_FLAG_HRPP) for the BVHs those scenes build with a
+// predictor, which approximates the reference's default output. Parity with the
+// reference's HRPP images cannot be pinned: they depend on thread timing.
 #include <math.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -45,7 +53,9 @@ void usage() {
             "      --cam-focus-dist <D>         [default: 10]\n"
             "      --cam-start-time <T>         [default: 0]\n"
             "      --cam-end-time <T>           [default: 0]\n"
-            "      --seed <N> --assets <DIR> --device <N> --devices <N> --pfm <FILE> --exact-bvh\n");
+            "      --seed <N> --assets <DIR> --device <N> --devices <N> --pfm <FILE> --exact-bvh\n"
+            "      --hrpp   hash-based ray path prediction on the scene's predictor BVHs (approximate;\n"
+            "               the reference's default for showcase / bunny / gargoyle / igea-hrpp)\n");
 }
 
 bool parse_f(const char* s, float* out) {
@@ -79,7 +89,7 @@ int main(int argc, char** argv) {
     float from[3] = {13.0f, 2.0f, 3.0f}, at[3] = {0.0f, 0.0f, 0.0f}, up[3] = {0.0f, 1.0f, 0.0f};
     float vfov = 20.0f, aperture = 0.0f, focus = 10.0f, t0 = 0.0f, t1 = 0.0f;
     std::string assets = default_assets(argv[0]), pfm;
-    bool exact = false;
+    bool exact = false, hrpp = false;
     for (int i = 1; i < argc; ++i) {
         std::string a = argv[i];
         auto need = [&](int n) {
@@ -124,6 +134,7 @@ int main(int argc, char** argv) {
         else if (a == "--assets") { need(1); assets = argv[++i]; }
         else if (a == "--pfm") { need(1); pfm = argv[++i]; }
         else if (a == "--exact-bvh") exact = true;
+        else if (a == "--hrpp") hrpp = true;
         else if (!a.empty() && a[0] == '-') { fprintf(stderr, "error: unexpected argument '%s'\n", a.c_str()); usage(); return 2; }
         else if (scene.empty()) scene = a;
         else { fprintf(stderr, "error: unexpected argument '%s'\n", a.c_str()); return 2; }
@@ -159,7 +170,7 @@ int main(int argc, char** argv) {
     p.tile_width = (uint32_t)tw;
     p.tile_height = (uint32_t)th;
     p.seed = seed;
-    p.flags = exact ? RT_FLAG_EXACT_BVH : 0u;
+    p.flags = (exact ? RT_FLAG_EXACT_BVH : 0u) | (hrpp ? RT_FLAG_HRPP : 0u);
     if (rt_scene_background(scene.c_str(), p.background) != RT_OK) {
         fprintf(stderr, "error: %s\n", rt_last_error());
         return 1;

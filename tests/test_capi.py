@@ -20,7 +20,7 @@ def declared_symbols():
 def test_every_declared_symbol_is_exported(rt):
     from raytracinginoneweekendinrust_amd import _capi
     syms = declared_symbols()
-    assert len(syms) == 19
+    assert len(syms) == 27
     out = subprocess.run(["nm", "-D", "--defined-only", _capi.LIB_PATH], capture_output=True, text=True, check=True)
     exported = set(re.findall(r"\sT\s(rt_[a-z0-9_]+)$", out.stdout, flags=re.M))
     missing = [s for s in syms if s not in exported]
@@ -38,7 +38,7 @@ def test_library_is_built_for_gfx950(rt):
 
 
 def test_abi_version(rt):
-    assert rt.lib.rt_abi_version() == 1
+    assert rt.lib.rt_abi_version() == 2
 
 
 def test_invalid_ir_is_reported_not_aborted(rt):

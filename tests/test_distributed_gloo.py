@@ -1,10 +1,13 @@
-"""The N>1 decomposition of bench.py, run with world_size-2 `gloo` ranks on CPU.
+"""The N>1 decomposition of bench.py, run with world_size-2/3 `gloo` ranks on CPU.
 
-Each rank computes its share with bench.rank_work() exactly as on the GPU box,
+Each rank computes its share with bench.rank_work() exactly as on the GPU box and
 renders it (the CPU oracle stands in for the device here — the GPU path's own
-shard/sample-range semantics are checked bit-exactly in test_gpu_parity.py),
-and the shares are exchanged with gloo collectives:
-  strong: the composed frame equals the single-process frame bit for bit;
+shard/sample-range semantics are checked bit-exactly in test_gpu_parity.py):
+  strong (bench's default): the shards go through the SAME FrameGather the bench
+          runs (shared-memory slots at rt_shard_offset, the gloo barrier, rank 0's
+          assembly), with torch restatements of rt_shard_pack / rt_shard_unpack in
+          place of the HIP kernels (tested on the device in test_gpu_boundary.py);
+          rank 0's frame equals the single-process frame bit for bit;
   weak:   the mean of the rank frames equals one render with N*spp samples up to
           float reassociation of the per-pixel sum (rtol 1e-6).
 """
@@ -28,6 +31,32 @@ def _free_port():
     return p
 
 
+def cpu_pack(img, w, h, r, n, packed, stream=0):
+    """Torch restatement of rt_shard_pack: blocks b = r, r+n, ... in order, 64 slots each."""
+    bx, nb = (w + 7) // 8, ((w + 7) // 8) * ((h + 7) // 8)
+    im = img.view(h, w, 3)
+    for k, b in enumerate(range(r, nb, n)):
+        x0, y0 = (b % bx) * 8, (b // bx) * 8
+        for p in range(64):
+            x, y = x0 + (p & 7), y0 + (p >> 3)
+            if x < w and y < h:
+                packed[(k * 64 + p) * 3: (k * 64 + p) * 3 + 3] = im[y, x]
+
+
+def cpu_unpack(packed_all, w, h, n, img, stream=0):
+    """Torch restatement of rt_shard_unpack: block b from shard b % n, slot b // n."""
+    import raytracinginoneweekendinrust_amd as rt
+    bx, nb = (w + 7) // 8, ((w + 7) // 8) * ((h + 7) // 8)
+    im = img.view(h, w, 3)
+    for b in range(nb):
+        base = rt.shard_offset(w, h, b % n, n) // 3 + (b // n) * 64
+        x0, y0 = (b % bx) * 8, (b // bx) * 8
+        for p in range(64):
+            x, y = x0 + (p & 7), y0 + (p >> 3)
+            if x < w and y < h:
+                im[y, x] = packed_all[(base + p) * 3: (base + p) * 3 + 3]
+
+
 def _worker(rank, world, port, scaling, q):
     import sys
     sys.path[:0] = [ROOT, os.path.join(ROOT, "oracle")]
@@ -40,9 +69,21 @@ def _worker(rank, world, port, scaling, q):
         cfg = rt.CONFIGS["C3"].scaled(40, 3)
         scene = rt.Scene.generate(cfg.scene, cfg.scene_seed)
         params, pixels = bench.rank_work(rt, cfg, rank, world, scaling)
-        img = np.zeros((cfg.height, cfg.width, 3), dtype=np.float32)
+        img = np.full((cfg.height, cfg.width, 3), -1.0, dtype=np.float32)  # other ranks' pixels: garbage
         _, cnt = orc.render(scene, cfg.camera(), params, out=img, threads=2)
         assert cnt["samples"] == pixels * cfg.spp
+        if scaling == "strong":  # the bench's gather path
+            from raytracinginoneweekendinrust_amd.frame_gather import FrameGather
+            g = FrameGather(cfg.width, cfg.height, rank, world, "cpu", pack=cpu_pack, unpack=cpu_unpack)
+            try:
+                full = g.gather(torch.from_numpy(img).reshape(-1))
+                if rank == 0:
+                    q.put((full.numpy().reshape(1, cfg.height, cfg.width, 3).copy(), cnt["seconds"]))
+                else:
+                    assert full is None
+            finally:
+                g.close()
+            return
         t = torch.from_numpy(img)
         gathered = [torch.zeros_like(t) for _ in range(world)]
         dist.all_gather(gathered, t)
@@ -76,10 +117,10 @@ def reference(rt, orc, spp_mult=1):
     return img
 
 
-def test_strong_scaling_shards_compose(rt, orc):
-    frames, wall = run("strong")
-    composed = frames.sum(axis=0)  # disjoint blocks; untouched pixels are 0
-    np.testing.assert_array_equal(composed, reference(rt, orc))
+@pytest.mark.parametrize("world", [2, 3])
+def test_strong_scaling_gather_assembles_the_frame(rt, orc, world):
+    frames, wall = run("strong", world)
+    np.testing.assert_array_equal(frames[0], reference(rt, orc))
     assert wall > 0
 
 

@@ -153,3 +153,25 @@ def test_oracle_bvh_order_matches_python_restatement(n, seed, orc):
     got = orc.bvh_order(keys, seed)
     want = _py_bvh_order([tuple(float(x) for x in r) for r in keys], seed)
     assert list(got) == want
+
+
+def test_prebuilt_tree_oracle_equals_flat_list(rt, orc):
+    """RT_OBJ_BVH_TREE in the oracle: a caller-built tree over random spheres and cubes (no
+    coincident surfaces, so no ties) gives the flat list's image (hittable.rs:100-118)."""
+    from tree_util import sphere_scene
+    cam = rt.Camera((13.0, 2.0, 3.0), (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), 20.0, 1.5, 0.1, 10.0, 0.0, 1.0)
+    p = rt.render_params(36, 24, 4, 8, background=(0.7, 0.8, 1.0))
+    a, ca = orc.render(sphere_scene(rt, with_tree=True), cam, p)
+    b, cb = orc.render(sphere_scene(rt, with_tree=False), cam, p)
+    np.testing.assert_array_equal(a, b)
+    assert ca["segments"] == cb["segments"] and ca["node_visits"] > 0 == cb["node_visits"]
+
+
+def test_camera_basis_oracle_equals_camera_new(rt, orc):
+    """oracle_render_camera with Camera::new's fields == oracle_render with its arguments."""
+    cfg = rt.CONFIGS["C3"].scaled(32, 2)
+    scene = rt.Scene.generate(cfg.scene, cfg.scene_seed)
+    p = rt.render_params(cfg.width, cfg.height, cfg.spp, cfg.depth, background=cfg.background())
+    a, _ = orc.render(scene, cfg.camera(), p)
+    b, _ = orc.render(scene, rt.CameraBasis.from_camera(cfg.camera()), p)
+    np.testing.assert_array_equal(a, b)

@@ -86,3 +86,24 @@ def test_obj_loader_fan_triangulates(rt, tmp_path):
     assert len(tris) == 3
     np.testing.assert_array_equal(tris["f"][0][:9], [0, 0, 0, 1, 0, 0, 1, 1, 0])
     np.testing.assert_array_equal(tris["f"][1][:9], [0, 0, 0, 1, 1, 0, 0, 1, 0])
+
+
+MULTI_OBJ = ("# two objects: tobj makes two models, main.rs:755 keeps models[0]\n"
+             "o first\nv 0 0 0\nv 100 0 0\nv 100 100 0\nv 0 100 0\nf 1 2 3 4\n"
+             "g second\nv 0 0 50\nv 100 0 50\nv 100 100 50\nf 5 6 7\nf -3 -2 -1\n")
+
+
+def test_obj_loader_keeps_models0_only(rt, tmp_path):
+    (tmp_path / "bunny_2000_scale.obj").write_text(MULTI_OBJ)
+    (tmp_path / "earthmap_1024x512.rgb8").write_bytes(b"")
+    n = rt.Scene.generate("bunny", 1, str(tmp_path)).nodes()
+    tris = n[n["kind"] == K.RT_OBJ_TRI]
+    assert len(tris) == 2  # the quad of `o first`, fan-triangulated; `g second` dropped
+    np.testing.assert_array_equal(tris["f"][1][:9], [0, 0, 0, 100, 100, 0, 0, 100, 0])
+
+
+def test_obj_group_without_faces_does_not_split(rt, tmp_path):
+    (tmp_path / "bunny_2000_scale.obj").write_text("g empty\nv 0 0 0\nv 1 0 0\nv 1 1 0\ng named\nf 1 2 3\n")
+    (tmp_path / "earthmap_1024x512.rgb8").write_bytes(b"")
+    n = rt.Scene.generate("bunny", 1, str(tmp_path)).nodes()
+    assert (n["kind"] == K.RT_OBJ_TRI).sum() == 1

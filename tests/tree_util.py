@@ -1,0 +1,99 @@
+"""Test helper: build reference-layout Bvh node arrays (src/bvh.rs:228-235) in Python
+with a split rule of the caller's own (not Bvh::new's), for RT_OBJ_BVH_TREE tests."""
+from __future__ import annotations
+
+import numpy as np
+
+from raytracinginoneweekendinrust_amd import _capi as K
+
+
+def prim_box(kind: int, f) -> tuple:
+    """Hittable::bounding_box in f32 like the reference (sphere.rs:105-109, cube.rs:95-97,
+    rectangle.rs:67-73 / 129-135 / 191-197, triangle.rs:94-107)."""
+    f = np.asarray(f, dtype=np.float32)
+    eps = np.float32(1.1920929e-07)
+    if kind == K.RT_OBJ_SPHERE:
+        return tuple(f[:3] - f[3]), tuple(f[:3] + f[3])
+    if kind == K.RT_OBJ_CUBE:
+        return tuple(f[:3]), tuple(f[3:6])
+    if kind == K.RT_OBJ_TRI:
+        p = f[:9].reshape(3, 3)
+        return tuple(p.min(axis=0) - eps), tuple(p.max(axis=0) + eps)
+    if kind == K.RT_OBJ_XY_RECT:
+        return (f[0], f[2], f[4] - eps), (f[1], f[3], f[4] + eps)
+    if kind == K.RT_OBJ_XZ_RECT:
+        return (f[0], f[4] - eps, f[2]), (f[1], f[4] + eps, f[3])
+    if kind == K.RT_OBJ_YZ_RECT:
+        return (f[4] - eps, f[0], f[2]), (f[4] + eps, f[1], f[3])
+    raise ValueError(kind)
+
+
+def build_tree(rt, objs, boxes, rng, split="random"):
+    """Nodes (postorder, root last, like BvhNode::new_helper pushes them) over `objs`
+    (IR node indices) with `boxes` [(min, max)]; returns (nodes, root_index).
+    split='random': random split point and random child order (no sorting at all);
+    'median-x': sorted on box min x, split at n/2."""
+    nodes = []
+
+    def union(a, b):
+        return (tuple(np.minimum(np.float32(a[0]), np.float32(b[0]))),
+                tuple(np.maximum(np.float32(a[1]), np.float32(b[1]))))
+
+    def rec(ids):
+        if len(ids) <= 2:
+            a = ids[0]
+            b = ids[1] if len(ids) == 2 else ids[0]
+            bx = union(boxes[a], boxes[b])
+            nodes.append(rt.BvhNode(objs[a], objs[b], K.RT_BVH_LEFT_HITTABLE | K.RT_BVH_RIGHT_HITTABLE, *bx))
+            return len(nodes) - 1, bx
+        if split == "median-x":
+            ids = sorted(ids, key=lambda i: boxes[i][0][0])
+            m = len(ids) // 2
+        else:
+            ids = list(ids)
+            rng.shuffle(ids)
+            m = int(rng.integers(1, len(ids)))
+        li, lb = rec(ids[:m])
+        ri, rb = rec(ids[m:])
+        bx = union(lb, rb)
+        nodes.append(rt.BvhNode(li, ri, 0, *bx))
+        me = len(nodes) - 1
+        nodes[li].parent = me
+        nodes[ri].parent = me
+        return me, bx
+
+    root, _ = rec(list(range(len(objs))))
+    return nodes, root
+
+
+def sphere_scene(rt, n=120, seed=5, tree="random", with_tree=True, cubes=20):
+    """Ground + n spheres (+ cubes) in a prebuilt tree (or a flat list when not with_tree)."""
+    rng = np.random.default_rng(seed)
+    b = rt.SceneBuilder()
+    world = rt.HittableList()
+    world.add(b.sphere((0.0, -1000.0, 0.0), 1000.0, b.lambertian(b.checker_from_color(10.0, (0.2, 0.3, 0.1),
+                                                                                       (0.9, 0.9, 0.9)))))
+    objs, boxes = [], []
+    glass = b.dielectric(1.5)
+    for i in range(n):
+        x, z = rng.uniform(-9, 9, 2)
+        r = float(rng.uniform(0.15, 0.4))
+        m = (b.metal(tuple(rng.uniform(0.5, 1, 3)), float(rng.uniform(0, 0.5))) if i % 4 == 0 else
+             glass if i % 9 == 0 else b.lambertian_from_color(tuple(rng.uniform(0, 1, 3))))
+        f = (float(x), r, float(z), r)
+        objs.append(b.sphere(f[:3], r, m))
+        boxes.append(prim_box(K.RT_OBJ_SPHERE, f))
+    for i in range(cubes):
+        x, z = rng.uniform(-9, 9, 2)
+        s = float(rng.uniform(0.2, 0.6))
+        f = (float(x), 0.0, float(z), float(x) + s, 2 * s, float(z) + s)
+        objs.append(b.cube(f[:3], f[3:], b.lambertian_from_color(tuple(rng.uniform(0, 1, 3)))))
+        boxes.append(prim_box(K.RT_OBJ_CUBE, f))
+    if with_tree:
+        nodes, root = build_tree(rt, objs, boxes, rng, tree)
+        world.add(b.bvh_tree(nodes, root))
+    else:
+        for o in objs:
+            world.add(o)
+    world.add(b.sphere((0.0, 1.0, 0.0), 1.0, glass))
+    return b.finish(world, "tree-spheres")

@@ -26,9 +26,12 @@ run() {  # run <name> <seconds> <cmd...>
     return 0
 }
 
+if [ -x tools/valu_rate ] && [ "$MODE" = "all" ]; then
+    run valu_rate 120 tools/valu_rate
+fi
 run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 if [ "$MODE" = "tests" ] || [ "$MODE" = "all" ]; then
-    run gpu_tests 1500 python -m pytest tests -m gpu -q -x --timeout 600 "$@"
+    run gpu_tests 1500 python -u -m pytest tests -m gpu -v -x --timeout 600 --timeout-method thread "$@"
 fi
 if [ "$MODE" = "bench" ] || [ "$MODE" = "all" ] || [ "$MODE" = "profile" ]; then
     run bench 900 python bench.py --steps 3 --warmup 1
