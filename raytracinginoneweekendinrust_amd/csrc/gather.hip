@@ -96,11 +96,12 @@ uint64_t rt_shard_offset(uint32_t width, uint32_t height, uint32_t rank, uint32_
 int rt_shard_pack(const float* d_image, uint32_t width, uint32_t height, uint32_t rank, uint32_t n, float* d_packed,
                   void* stream) {
     rthost::clear_error();
-    if (!d_image || !d_packed || n == 0 || rank >= n || width == 0 || height == 0)
-        return rthost::set_error(RT_ERR_INVALID, "rt_shard_pack: NULL buffer, empty image or rank >= n");
+    if (n == 0 || rank >= n || width == 0 || height == 0)
+        return rthost::set_error(RT_ERR_INVALID, "rt_shard_pack: empty image or rank >= n");
     const Grid g = grid_of(width, height);
     const uint64_t slots = blocks_of(g.nb, rank, n) * 64u;
-    if (slots == 0) return RT_OK;
+    if (slots == 0) return RT_OK;  // a rank without blocks (n > blocks) ships nothing
+    if (!d_image || !d_packed) return rthost::set_error(RT_ERR_INVALID, "rt_shard_pack: NULL buffer");
     (void)hipGetLastError();
     hipLaunchKernelGGL(shard_pack, dim3(launch_blocks(slots)), dim3(256), 0, (hipStream_t)stream, d_image, width,
                        height, g.bx, rank, n, slots, d_packed);
