@@ -426,7 +426,8 @@ RT_DEV bool tri_t(f4 t0, f4 t1, f4 t2, const Ray& r, float tmin, float tmax, flo
 // the BVH code, showcase 2.5% faster without the triangle code).
 // kFDeep: a BVH stack deeper than kStackLdsMax entries; kFLeafRM: BVH leaves that are
 // rects or moving spheres (BVH leaf tests otherwise handle spheres, cubes, triangles).
-constexpr uint32_t kFBvh = 1u, kFTri = 2u, kFRuns = 4u, kFDeep = 8u, kFLeafRM = 16u, kFAll = 31u;
+constexpr uint32_t kFBvh = 1u, kFTri = 2u, kFRuns = 4u, kFDeep = 8u, kFLeafRM = 16u, kFMarble = 32u, kFAll = 63u;
+// kFMarble: Marble textures, whose Perlin turbulence the whole wave evaluates together (turbulence_wave).
 [[maybe_unused]] constexpr uint32_t kStackLdsMax = 19u;  // LDS stack entries per lane at most (9.5 KB per wave: 16 waves/CU)
 // One leaf (primitive or cube). tmax = closest so far; a hit with t == closest is
 // accepted, so later candidates win ties exactly like hittable.rs:110-116.
@@ -1403,7 +1404,98 @@ __device__ __noinline__ double turbulence(const uint8_t* tabs, double px, double
     double zd = pz + fbm_get(tabs, 2u, px + 53820.0 / 65536.0, py + 11213.0 / 65536.0, pz + 44845.0 / 65536.0) * power;
     return perlin3(tabs, xd, yd, zd);
 }
-RT_DEV V tex_value(const DevScene& S, uint32_t tid, float u, float v, V p) {
+// The turbulence noise 0.8.2 computes for Marble (marble.rs:23-29) at p for every lane
+// with `need`, evaluated by the whole wave together; all 64 lanes must call it
+// (convergent). Sequentially it is 19 Perlin evaluations per lane, and a Marble hit
+// is rare (3.4 lanes of 64 on C3): here the 18 fbm octaves (3 fbm x 6, independent
+// of each other) of up to 3 requesting lanes are spread over 54 lanes, each lane
+// evaluating one perlin3 with the same operations fbm_get applies for that octave
+// (the point scaled by the lacunarity o times, then signal * persist, a power of
+// two), the requester sums its octaves in fbm_get's order, and only the final
+// perlin3 runs per lane. Every value is the one turbulence() computes, bit for bit.
+// `tab` = the Marble's first permutation table (DevTexture::a).
+#ifdef RT_TURB_NOINLINE
+__device__ __noinline__
+#else
+__device__ __forceinline__
+#endif
+double turbulence_wave(const uint8_t* perm, bool need, V p, uint32_t tab) {
+    const uint32_t lane = __lane_id();
+    unsigned long long pending = __ballot(need);
+    double xd = 0.0, yd = 0.0, zd = 0.0;
+    const double lac = 3.141592653589793 * 2.0 / 3.0;
+    double denom = 0.0, pw = 1.0;
+    for (int i = 1; i <= 6; ++i) {
+        pw = pw * 0.5;
+        denom = denom + pw;
+    }
+    const double scale_factor = 1.0 / denom;
+    const uint32_t j = lane / 18u, k = lane - j * 18u, f = k / 6u, o = k - f * 6u;  // this lane's (requester, fbm, octave)
+    while (pending) {
+        uint32_t req[3] = {0u, 0u, 0u}, nreq = 0u;
+        for (; nreq < 3u && pending; ++nreq) {
+            req[nreq] = (uint32_t)__builtin_ctzll(pending);
+            pending &= pending - 1ull;
+        }
+        const uint32_t src = j == 0u ? req[0] : (j == 1u ? req[1] : req[2]);
+        const float qx = __shfl(p.x, (int)src), qy = __shfl(p.y, (int)src), qz = __shfl(p.z, (int)src);
+        const uint32_t qt = __shfl(tab, (int)src);
+        double sig = 0.0;
+        if (j < nreq) {  // fbm_get(tabs, f, p + offset_f) octave o
+            const double ox = f == 0u ? 12414.0 / 65536.0 : (f == 1u ? 26519.0 / 65536.0 : 53820.0 / 65536.0);
+            const double oy = f == 0u ? 65124.0 / 65536.0 : (f == 1u ? 18128.0 / 65536.0 : 11213.0 / 65536.0);
+            const double oz = f == 0u ? 31337.0 / 65536.0 : (f == 1u ? 60493.0 / 65536.0 : 44845.0 / 65536.0);
+            double x = (double)qx + ox, y = (double)qy + oy, z = (double)qz + oz;
+            x = x * 1.0; y = y * 1.0; z = z * 1.0;
+            double persist = 1.0;
+            for (uint32_t i = 0; i < o; ++i) {
+                persist = persist * 0.5;
+                x = x * lac; y = y * lac; z = z * lac;
+            }
+            sig = perlin3(perm + 256u * (qt + 1u + f + o), x, y, z) * persist;
+        }
+        // requester r of this round sums its 18 signals in fbm_get's order
+        int mine = -1;
+        for (uint32_t r = 0; r < nreq; ++r)
+            if (lane == req[r]) mine = (int)r;
+        double fb[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+        for (uint32_t ff = 0; ff < 3u; ++ff) {
+            double result = 0.0;
+#pragma unroll
+            for (uint32_t oo = 0; oo < 6u; ++oo) {
+                const int from = (mine < 0 ? 0 : mine) * 18 + (int)(ff * 6u + oo);
+                const double v = __shfl(sig, from);
+                result = result + v;
+            }
+            fb[ff] = result * scale_factor;
+        }
+        if (mine >= 0) {
+            const double power = 1.0;
+            xd = (double)p.x + fb[0] * power;
+            yd = (double)p.y + fb[1] * power;
+            zd = (double)p.z + fb[2] * power;
+        }
+    }
+    return need ? perlin3(perm + 256u * tab, xd, yd, zd) : 0.0;
+}
+
+// The texture a chain of Checkers (checker.rs:27-37) resolves to at p: what tex_value
+// would evaluate. Side-effect free, so tex_value may start from the result (same bits).
+RT_DEV uint32_t tex_resolve(const DevScene& S, uint32_t tid, V p) {
+    for (;;) {
+        const DevTexture* T = S.texs + tid;
+        if (T->kind != rtdev::kTexChecker) return tid;
+        float sc = T->scale;
+        float sines = rt_sinf(sc * p.x) * rt_sinf(sc * p.y) * rt_sinf(sc * p.z);
+        tid = sign_negative(sines) ? T->b : T->a;
+    }
+}
+
+// kTurb: a Marble reached by this evaluation takes `turb` (turbulence_wave's value at the
+// same p) instead of computing the turbulence itself.
+template <bool kTurb = false>
+RT_DEV V tex_value(const DevScene& S, uint32_t tid, float u, float v, V p, double turb = 0.0) {
     for (;;) {
         const DevTexture* T = S.texs + tid;
         uint32_t kind = T->kind;
@@ -1418,7 +1510,7 @@ RT_DEV V tex_value(const DevScene& S, uint32_t tid, float u, float v, V p) {
         }
         if (kind == rtdev::kTexMarble) {  // marble.rs:23-29
             PROF_T0(pm);
-            double n = turbulence(S.perm + 256u * T->a, (double)p.x, (double)p.y, (double)p.z);
+            double n = kTurb ? turb : turbulence(S.perm + 256u * T->a, (double)p.x, (double)p.y, (double)p.z);
             float s = 0.5f * (1.0f + rt_sinf(T->scale * p.z + 10.0f * (float)n));
             PROF_ADD(kPrMarble, pm);
             return mk(s, s, s);
@@ -1454,8 +1546,9 @@ RT_DEV bool near_zero(V v) {  // utils.rs:5-7
     const float eps = 1.1920929e-07f;
     return __builtin_fabsf(v.x) < eps && __builtin_fabsf(v.y) < eps && __builtin_fabsf(v.z) < eps;
 }
+template <bool kTurb = false>
 RT_DEV bool scatter(const DevScene& S, const DevMaterial& m, const Ray& r, const Rec& rec, Rng& g, const Key& k,
-                    V& att, Ray& sc) {
+                    V& att, Ray& sc, uint32_t tex = 0u, double turb = 0.0) {
     sc.o = rec.p;
     sc.time = r.time;
     // Lambertian, Metal and Isotropic each draw exactly one in_unit_sphere() and
@@ -1471,7 +1564,7 @@ RT_DEV bool scatter(const DevScene& S, const DevMaterial& m, const Ray& r, const
         V dir = rec.n + normalize(rs);
         if (near_zero(dir)) dir = rec.n;
         sc.d = dir;
-        att = tex_value(S, m.tex, rec.u, rec.v, rec.p);
+        att = tex_value<kTurb>(S, kTurb ? tex : m.tex, rec.u, rec.v, rec.p, turb);
         PROF_ADD(kPrLambert, pb);
         return true;
     }
@@ -1508,7 +1601,7 @@ RT_DEV bool scatter(const DevScene& S, const DevMaterial& m, const Ray& r, const
     if (m.kind == rtdev::kMatIsotropic) {  // isotropic.rs:31-43
         PROF_T0(ps);
         sc.d = rs;
-        att = tex_value(S, m.tex, rec.u, rec.v, rec.p);
+        att = tex_value<kTurb>(S, kTurb ? tex : m.tex, rec.u, rec.v, rec.p, turb);
         PROF_ADD(kPrIso, ps);
         return true;
     }
@@ -1682,6 +1775,48 @@ RT_DEV bool take_sample(ItemPool& pool, bool want, const DevCamera& C, const Dev
 // The end of a segment whose list walk is complete (ray.rs:43-61): background,
 // or HitRecord + emit + scatter. Returns true when the path ends; its radiance is
 // then stored in the sample buffer.
+// The same end of a segment with the HitRecord already built (rec, when any) and the
+// material's texture already resolved through its Checkers (tex) for the instances
+// that evaluate Marble turbulence wave-wide: the caller passed `turb` from
+// turbulence_wave for a Marble hit (kFMarble).
+RT_DEV bool finish_segment_rec(const DevScene& S, const DevParams& P, const ChunkParams& Q, const Key& k,
+                               float* __restrict__ sbuf, bool any, const Rec& rec, uint32_t tex, double turb, Ray& ray,
+                               V& L, V& T, uint32_t& depth, Rng& g, uint32_t pixel, uint32_t s_local) {
+    PROF_T0(pg);
+    bool done;
+    if (!any) {
+        L = L + T * mk(P.bg[0], P.bg[1], P.bg[2]);
+        done = true;
+    } else {
+        const DevMaterial m = S.mats[rec.mat];
+        PROF_T0(pm);
+        V em = m.kind == rtdev::kMatLight ? tex_value<true>(S, tex, rec.u, rec.v, rec.p, turb) : mk(0.0f, 0.0f, 0.0f);
+        L = L + T * em;
+        PROF_ADD(kPrEmit, pm);
+        V att;
+        Ray sc;
+        PROF_T0(ps);
+        bool scattered = scatter<true>(S, m, ray, rec, g, k, att, sc, tex, turb);
+        PROF_ADD(kPrScatter, ps);
+        if (scattered) {
+            T = T * att;
+            ray = sc;
+            depth -= 1u;
+            done = depth == 0u;
+        } else {
+            done = true;
+        }
+    }
+    if (done) {
+        float* o = sbuf + ((size_t)s_local * Q.npix + pixel) * 3u;
+        o[0] = L.x;
+        o[1] = L.y;
+        o[2] = L.z;
+    }
+    PROF_ADD(kPrSegment, pg);
+    return done;
+}
+
 template <uint32_t kF = kFAll>
 RT_DEV bool finish_segment(const DevScene& S, const DevParams& P, const ChunkParams& Q, const Key& k,
                            float* __restrict__ sbuf, bool any, uint32_t he, uint32_t hc, float t, Ray& ray, V& L, V& T,
@@ -1804,7 +1939,55 @@ __global__ __launch_bounds__(64, kWaves) void trace_samples(DevScene Sg, DevCame
         }
         PROF_ADD(kPrRefill, pr);
         if (__ballot(has) == 0ull) break;  // pool exhausted and every path finished
-        if (has) {
+        if constexpr ((kF & kFMarble) != 0u) {
+            // world walk and HitRecord per lane, then the Marble turbulence of every lane that
+            // needs it evaluated by the whole (converged) wave, then emit / scatter per lane
+            bool shade = false, any = false;
+            Rec rec;
+            rec.p = mk(0.0f, 0.0f, 0.0f);
+            uint32_t tex = 0u, tab = 0u;
+            bool marble = false;
+            if (has) {
+                nseg_sample += 1u;
+                float t;
+                uint32_t he = 0, hc = 0;
+                bool replay = false;
+                PROF_T0(pw);
+                any = world_hit<kKind, kF>(S, P.prune_delta, ray, g, k, t, he, hc, stk, mode, replay);
+                PROF_ADD(kPrWorld, pw);
+                if (kKind == 0 && replay) {  // hand the sample to the reference kernel
+                    unsigned idx = atomicAdd(&ctr->replay_count, 1u);
+                    if (idx < kReplayCap) replay_list[idx] = ReplayItem{pixel, s_local};
+                    has = false;
+                } else {
+                    shade = true;
+                    if (any) {
+                        PROF_T0(pc);
+                        make_record<kF>(S, he, hc, t, ray, rec);
+                        PROF_ADD(kPrRecord, pc);
+                        const DevMaterial& m = S.mats[rec.mat];
+                        if (m.kind == rtdev::kMatLight || m.kind == rtdev::kMatLambertian ||
+                            m.kind == rtdev::kMatIsotropic) {
+                            tex = tex_resolve(S, m.tex, rec.p);
+                            const DevTexture& tx = S.texs[tex];
+                            marble = tx.kind == rtdev::kTexMarble;
+                            tab = tx.a;
+                        }
+                    }
+                }
+            }
+            PROF_T0(pmw);
+            double turb = 0.0;
+#ifdef RT_TURB_NOINLINE
+            if (__ballot(marble))
+#endif
+                turb = turbulence_wave(S.perm, marble, rec.p, tab);
+            PROF_ADD(kPrMarble, pmw);
+            if (shade && finish_segment_rec(S, P, Q, k, sbuf, any, rec, tex, turb, ray, L, T, depth, g, pixel, s_local)) {
+                has = false;
+                nseg += nseg_sample;
+            }
+        } else if (has) {
             nseg_sample += 1u;
             float t;
             uint32_t he = 0, hc = 0;
@@ -1888,6 +2071,7 @@ __global__ void numeric_eval(int op, const double* a, const double* b, double* o
 // BVH-only and the sphere-run presets, built with the memory-clause scheduler.
 void* rt_mc_trace_instance(uint32_t preset) {
     if (preset == kFBvh) return reinterpret_cast<void*>(trace_samples<0, 4, kFBvh>);
+    if (preset == (kFBvh | kFMarble)) return reinterpret_cast<void*>(trace_samples<0, 4, kFBvh | kFMarble>);
     if (preset == kFRuns) return reinterpret_cast<void*>(trace_samples<0, 4, kFRuns>);
     return nullptr;
 }
@@ -1988,7 +2172,7 @@ using TraceKernel = void (*)(DevScene, DevCamera, DevParams, ChunkParams, float*
 template <int kWaves, uint32_t kF>
 TraceKernel preset_instance() {
 #ifdef RT_SPLIT_MC
-    if constexpr (kWaves == 4 && (kF == kFBvh || kF == kFRuns))
+    if constexpr (kWaves == 4 && (kF == kFBvh || kF == (kFBvh | kFMarble) || kF == kFRuns))
         return reinterpret_cast<TraceKernel>(rt_mc_trace_instance(kF));
     else
 #endif
@@ -1999,6 +2183,7 @@ TraceKernel fast_instance(uint32_t features) {
     if (features == 0u) return preset_instance<kWaves, 0u>();
     if ((features & ~kFRuns) == 0u) return preset_instance<kWaves, kFRuns>();
     if ((features & ~kFBvh) == 0u) return preset_instance<kWaves, kFBvh>();
+    if ((features & ~(kFBvh | kFMarble)) == 0u) return preset_instance<kWaves, kFBvh | kFMarble>();
     if ((features & ~(kFBvh | kFTri | kFDeep)) == 0u) return preset_instance<kWaves, kFBvh | kFTri | kFDeep>();
     return preset_instance<kWaves, kFAll>();
 }
@@ -2141,6 +2326,10 @@ int rt_scene_upload(const rt_scene_desc* desc, int device, rt_scene_handle* out)
     d.hrpp_npred = hs.num_predictors;
     s->coord_bound = hs.coord_bound;
     s->features = (hs.tri.empty() ? 0u : kFTri) | (hs.bvh_rect_msph ? kFLeafRM : 0u);
+#ifndef RT_NO_MARBLE_COOP
+    for (const rtdev::DevTexture& t : hs.texs)
+        if (t.kind == rtdev::kTexMarble) s->features |= kFMarble;
+#endif
 #ifndef RT_LEAF_AUDIT  // (the audit build replays traversals on the same LDS stack: no spill area)
     {  // deep BVHs: the LDS stack keeps kStackLdsMax entries, HBM the rest
         uint32_t cap = kStackLdsMax;
