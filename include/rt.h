@@ -332,6 +332,15 @@ int rt_scene_background(const char* name, float rgb[3]);
 int rt_device_numeric_eval(int op, const double* a, const double* b, double* out,
                            uint32_t n);
 
+/* Device known answers (diagnostic): the kernel's own primitives evaluated on the GPU
+ * for n cases, two floats out per case. op 0: Aabb::hit (aabb.rs:28-41) as the
+ * reference-exact slab test, op 1: the same box through the fast kernel's packed
+ * four-child test — in: 14 floats per case (min[3], max[3], origin[3], direction[3],
+ * t_min, t_max), out: (hit 1/0, entry t); op 2: Sphere::get_uv (sphere.rs:41-46) —
+ * in: p[3], out: (u, v); op 3: Sphere::hit's root (sphere.rs:49-103) — in: center[3],
+ * radius, origin[3], direction[3], t_min, t_max, out: (hit 1/0, t). */
+int rt_device_kat(int op, const float* in, float* out, uint32_t n);
+
 #ifdef __cplusplus
 }
 #endif

@@ -120,6 +120,7 @@ SIGNATURES = [
     ("rt_shard_offset", C.c_uint64, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]),
     ("rt_shard_pack", C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p]),
     ("rt_shard_unpack", C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p]),
+    ("rt_device_kat", C.c_int, [C.c_int, C.POINTER(C.c_float), C.POINTER(C.c_float), C.c_uint32]),
 ]
 
 

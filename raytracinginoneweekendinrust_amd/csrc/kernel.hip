@@ -66,6 +66,9 @@ enum ProfRegion : uint32_t {
 // from DevParams::tune (RT_TUNE environment variable, diagnostics / A-B runs).
 constexpr uint32_t kModeExact = 1u, kModeNoLeafBoxes = 2u, kModeNoPermLds = 32u, kModeW3 = 64u,
                    kModeNoPretest = 128u, kModeReplayRef = 1u << 16;  // ReplayRef: the replay pass runs trace_samples<1>
+// EXPERIMENT ONLY (RT_TUNE, not exact): closest-hit pruning also on BVHs the proof does not
+// cover (triangles, moving spheres), to measure what an exact bound for them could gain.
+constexpr uint32_t kModePruneAllExp = 1u << 20;
 #ifdef RT_ABLATE
 // Ablation build (librtamd_ablate.so, diagnostics only): RT_TUNE bits that run a
 // piece of work twice (results of the copy discarded through an opaque test),
@@ -906,7 +909,7 @@ RT_DEV bool bvh_hit(const DevScene& S, float delta, uint32_t root, const Ray& r,
             return false;
         }
     }
-    const bool prune = (__float_as_uint(wrapper[7].w) & rtdev::kBvhPrunable) != 0u;
+    const bool prune = (__float_as_uint(wrapper[7].w) & rtdev::kBvhPrunable) != 0u || (mode & kModePruneAllExp);
     const float dmi = delta * fmaxf(fmaxf(__builtin_fabsf(inv.x), __builtin_fabsf(inv.y)), __builtin_fabsf(inv.z));
     const bool leaf_boxes = prune && !(mode & kModeNoLeafBoxes);
     bool any = false;
@@ -2064,6 +2067,49 @@ __global__ void numeric_eval(int op, const double* a, const double* b, double* o
     out[i] = r;
 }
 
+// Device known-answer evaluation (rt_device_kat): the kernel's own primitives on
+// caller-supplied inputs, for the reference's unit tests run on the GPU.
+__global__ void kat_eval(int op, const float* __restrict__ in, float* __restrict__ out, uint32_t n) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float r0 = 0.0f, r1 = 0.0f;
+    if (op == 0 || op == 1) {  // Aabb::hit (aabb.rs:28-41): min, max, origin, direction, t_min, t_max
+        const float* a = in + 14u * i;
+        Ray r;
+        r.o = mk(a[6], a[7], a[8]);
+        r.d = mk(a[9], a[10], a[11]);
+        r.time = 0.0f;
+        const V inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
+        if (op == 0) {  // the reference-exact slab test (bvh_hit_reference, the BVH root test)
+            float te = 0.0f;
+            r0 = slab(a[0], a[1], a[2], a[3], a[4], a[5], r, inv, a[12], a[13], te) ? 1.0f : 0.0f;
+            r1 = te;
+        } else {  // the packed four-child test of the fast kernel, box in slot 0, empty slots 1-3
+            const float E = kInf;
+            f4 mnx{a[0], E, E, E}, mny{a[1], E, E, E}, mnz{a[2], E, E, E};
+            f4 mxx{a[3], -E, -E, -E}, mxy{a[4], -E, -E, -E}, mxz{a[5], -E, -E, -E};
+            float key[4];
+            child_keys4(mnx, mny, mnz, mxx, mxy, mxz, r, inv, a[12], a[13], kInf, 0.0f, key);
+            r0 = key[0] != kInf ? 1.0f : 0.0f;
+            r1 = key[0];
+        }
+    } else if (op == 2) {  // Sphere::get_uv (sphere.rs:41-46)
+        const float* a = in + 3u * i;
+        sphere_uv(mk(a[0], a[1], a[2]), r0, r1);
+    } else if (op == 3) {  // Sphere::hit's root (sphere.rs:49-103): center, radius, origin, direction, t_min, t_max
+        const float* a = in + 12u * i;
+        Ray r;
+        r.o = mk(a[4], a[5], a[6]);
+        r.d = mk(a[7], a[8], a[9]);
+        r.time = 0.0f;
+        float t = 0.0f;
+        r0 = sphere_t(f4{a[0], a[1], a[2], a[3]}, to_d(r), a[10], a[11], t) ? 1.0f : 0.0f;
+        r1 = t;
+    }
+    out[2u * i] = r0;
+    out[2u * i + 1u] = r1;
+}
+
 }  // namespace
 
 #ifdef RT_INSTANCES_TU
@@ -2542,7 +2588,18 @@ int rt_render_launch_camera(rt_scene_handle s, const rt_camera* camera, const rt
     // Sample buffer: chunks of whole sample ranges (the per-pixel sum stays in order).
     const uint64_t npix = (uint64_t)p->width * p->height;
     const uint64_t per_sample = npix * 3u * sizeof(float);
+    // One launch per frame whenever HBM allows (each chunk ends with its own drain tail):
+    // up to 40% of the free HBM, at least 8 GiB (C4's 1000-spp frame needs 24.9 GB, C5's 49.8 GB)
     uint64_t budget = 8192ull << 20;
+    {
+        size_t free_b = 0, total_b = 0;
+        if (s->sbuf_bytes >= per_sample * p->samples_per_pixel) {
+            budget = s->sbuf_bytes;  // the buffer already holds the whole frame
+        } else if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) {
+            const uint64_t avail = (uint64_t)((double)(free_b + s->sbuf_bytes) * 0.4);
+            if (avail > budget) budget = avail;
+        }
+    }
     if (const char* env = getenv("RT_SAMPLE_BUFFER_MB")) budget = strtoull(env, nullptr, 10) << 20;
     uint64_t max_s = budget / per_sample;
     if (max_s < 1) max_s = 1;
@@ -2896,6 +2953,31 @@ int rt_scene_trace_time(rt_scene_handle s, double* total_ms, uint64_t* launches,
         return rthost::set_error(RT_ERR_INVALID, "more than 256 launches since the last reset: timing incomplete");
     }
     if (reset) s->ev_count = 0;
+    return RT_OK;
+}
+
+int rt_device_kat(int op, const float* in, float* out, uint32_t n) {
+    rthost::clear_error();
+    if (!in || !out) return rthost::set_error(RT_ERR_INVALID, "NULL argument");
+    if (op < 0 || op > 3) return rthost::set_error(RT_ERR_INVALID, "unknown KAT op");
+    int rc = check_device(0);
+    if (rc) return rc;
+    if (n == 0) return RT_OK;
+    DeviceGuard g(0);
+    const size_t in_floats = (size_t)n * (op <= 1 ? 14u : (op == 2 ? 3u : 12u)), out_floats = (size_t)n * 2u;
+    float *din = nullptr, *dout = nullptr;
+    hipError_t e = hipMalloc(&din, in_floats * sizeof(float));
+    if (e == hipSuccess) e = hipMalloc(&dout, out_floats * sizeof(float));
+    if (e == hipSuccess) e = hipMemcpy(din, in, in_floats * sizeof(float), hipMemcpyHostToDevice);
+    if (e == hipSuccess) {
+        (void)hipGetLastError();
+        hipLaunchKernelGGL(kat_eval, dim3((n + 63u) / 64u), dim3(64), 0, nullptr, op, din, dout, n);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpy(out, dout, out_floats * sizeof(float), hipMemcpyDeviceToHost);
+    if (din) (void)hipFree(din);
+    if (dout) (void)hipFree(dout);
+    if (e != hipSuccess) return hip_fail(e, "kat_eval");
     return RT_OK;
 }
 

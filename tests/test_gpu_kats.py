@@ -1,0 +1,69 @@
+"""The reference's own unit tests and doc-comment known answers, run on the DEVICE
+through the kernel's own primitives (rt_device_kat), not only on the oracle:
+
+  src/aabb.rs:73-97    Aabb::hit `hits` / `misses` — exact slab test (op 0) and, for the
+                       rays the fast kernel traverses (finite non-zero 1/d), the packed
+                       four-child test (op 1)
+  src/geometry/sphere.rs:37-40   Sphere::get_uv's six examples (op 2)
+
+plus dense random cases against the oracle restatement bit for bit (aabb_hit for the
+boxes, the uv formulas) and the fast test against the exact one. (aabb.rs:99-140, the
+union tests, exercise host code the device never runs: test_reference_units.py.)
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def test_aabb_rs_hits_and_misses_on_device(rt):  # aabb.rs:73-97
+    hits = [-1, -1, 1, 1, 1, 2, 0, 0, 0, 0, 0, 1, 0.0, 5.0]
+    misses = [1, 1, 1, 2, 2, 2, 0, 0, 0, 0, 0, 1, 0.0, 5.0]
+    r = rt.device_kat(0, [hits, misses])
+    assert r[0, 0] == 1.0 and r[1, 0] == 0.0
+
+
+def test_aabb_rs_cases_through_the_fast_box_test(rt):
+    # the same boxes, rays tilted off the axes (the fast kernel only takes rays with
+    # 0 < |1/d| < inf on every axis; the axis-parallel ones go to the exact kernel)
+    hits = [-1, -1, 1, 1, 1, 2, 0, 0, 0, 1e-3, 1e-3, 1, 0.0, 5.0]
+    misses = [1, 1, 1, 2, 2, 2, 0, 0, 0, 1e-3, 1e-3, 1, 0.0, 5.0]
+    r = rt.device_kat(1, [hits, misses])
+    assert r[0, 0] == 1.0 and r[1, 0] == 0.0
+
+
+@pytest.mark.parametrize("p,uv", [((1, 0, 0), (0.5, 0.5)), ((-1, 0, 0), (0.0, 0.5)), ((0, 1, 0), (0.5, 1.0)),
+                                   ((0, -1, 0), (0.5, 0.0)), ((0, 0, 1), (0.25, 0.5)), ((0, 0, -1), (0.75, 0.5))])
+def test_sphere_rs_get_uv_examples_on_device(rt, orc, p, uv):  # sphere.rs:37-40
+    got = rt.device_kat(2, [p])[0]
+    assert got[0] == pytest.approx(uv[0], abs=1e-6) and got[1] == pytest.approx(uv[1], abs=1e-6)
+    np.testing.assert_array_equal(got, np.array(orc.sphere_uv(p), dtype=np.float32))
+
+
+def test_random_boxes_device_equals_oracle_and_fast_equals_exact(rt, orc):
+    rng = np.random.default_rng(9)
+    n = 20000
+    mn = rng.uniform(-10, 10, (n, 3)).astype(np.float32)
+    mx = mn + rng.uniform(0, 5, (n, 3)).astype(np.float32)
+    o = rng.uniform(-15, 15, (n, 3)).astype(np.float32)
+    # aimed near the box so that about half the rays hit
+    d = ((mn + mx) / 2 - o + rng.normal(scale=1.0, size=(n, 3))).astype(np.float32)
+    t = np.stack([rng.uniform(0, 0.3, n), rng.uniform(0.5, 3, n)], axis=1).astype(np.float32)
+    cases = np.concatenate([mn, mx, o, d, t], axis=1)
+    exact = rt.device_kat(0, cases)
+    fast = rt.device_kat(1, cases)
+    want = np.array([orc.aabb_hit(c[0:3], c[3:6], c[6:9], c[9:12], c[12], c[13]) for c in cases[:4000]])
+    np.testing.assert_array_equal(exact[:4000, 0] == 1.0, want)
+    np.testing.assert_array_equal(fast[:, 0], exact[:, 0])
+    hit = exact[:, 0] == 1.0
+    assert 0.2 < hit.mean() < 0.9, hit.mean()
+    np.testing.assert_array_equal(fast[hit, 1], np.minimum(exact[hit, 1], np.float32(3.4028235e38)))
+
+
+def test_random_sphere_uv_device_equals_oracle(rt, orc):
+    rng = np.random.default_rng(4)
+    p = rng.normal(size=(3000, 3))
+    p = (p / np.linalg.norm(p, axis=1, keepdims=True)).astype(np.float32)
+    got = rt.device_kat(2, p)
+    want = np.array([orc.sphere_uv(q) for q in p], dtype=np.float32)
+    np.testing.assert_array_equal(got, want)

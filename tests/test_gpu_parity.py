@@ -196,16 +196,18 @@ def test_c3_full_resolution_one_spp_matches_oracle(rt, orc):
     np.testing.assert_array_equal(got, want)
 
 
-def test_c3_full_workload_subsample_matches_oracle(rt, orc):
-    # the full 1200x800x500spp render on the GPU, checked bit-exactly on a 1/256
-    # block shard rendered by the oracle at the same full spp
-    cfg = rt.CONFIGS["C3"]
+@pytest.mark.parametrize("cfg_name,shard", [("C3", 101), ("C4", 77), ("C5", 200)])
+def test_full_workload_subsample_matches_oracle(cfg_name, shard, rt, orc):
+    # the full-size render on the GPU (C3 1200x800x500, C4 1920x1080x1000 over the
+    # 20k-triangle mesh, C5 1920x1080x2000 with the media), checked bit-exactly on a
+    # 1/256 block shard rendered by the oracle at the same full spp and depth
+    cfg = rt.CONFIGS[cfg_name]
     scene = rt.Scene.generate(cfg.scene, cfg.scene_seed)
     params = rt.render_params(cfg.width, cfg.height, cfg.spp, cfg.depth, background=cfg.background())
     got, st = gpu_render(rt, scene, cfg.camera(), params)
-    assert st["samples"] == 1200 * 800 * 500
+    assert st["samples"] == cfg.width * cfg.height * cfg.spp
     sub = rt.render_params(cfg.width, cfg.height, cfg.spp, cfg.depth, background=cfg.background(),
-                           shard_index=101, shard_count=256)
+                           shard_index=shard, shard_count=256)
     want = np.full_like(got, np.nan)
     orc.render(scene, cfg.camera(), sub, out=want)
     mask = ~np.isnan(want[..., 0])
