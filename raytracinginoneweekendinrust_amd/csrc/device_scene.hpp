@@ -37,6 +37,11 @@ constexpr uint32_t kLeafMedium = 6u;   // hit identifier of a ConstantMedium sca
 constexpr uint32_t kChildEmpty = 0xffffffffu;  // second child of a 1-object node (bvh.rs:261-264)
 constexpr uint32_t kMaxIndex = 0x0fffffffu;
 constexpr uint32_t kBvhPrunable = 1u;  // wrapper-node flag: closest-hit box pruning is exact for this BVH
+// BVH2 wrapper flag (nodes2 wrapper row 3 .w): every leaf is a Tri. Möller-Trumbore
+// (triangle.rs:32-92) rejects any ray with a NaN origin or direction component (a NaN
+// reaches t, and !(t > EPSILON) rejects it), so such a BVH returns no hit for that ray
+// whatever its boxes do; bvh_hit_reference answers at once instead of visiting every node.
+constexpr uint32_t kBvh2TriOnly = 1u;
 constexpr uint32_t kBvhWidth = 4u;     // children per BVH node (collapsed from the reference BVH2)
 constexpr uint32_t kBvhNodeF4 = 8u;    // f4 records per BVH node
 // A BVH4 node holds either only leaves (the 1-2 leaf children of one reference
@@ -111,7 +116,8 @@ static_assert(sizeof(DevTexture) == 32, "DevTexture layout");
 //          node whose slot 0 is the root; the wrapper's rank[3] holds kBvhPrunable
 //          when every leaf is a Sphere/Rect/Cube, its rank[2] the BVH2 wrapper.
 //   node2: 64 B reference BVH2 node: (Lmin, Lmax.x) (Lmax.yz, Rmin.xy) (Rmin.z,
-//          Rmax) (left, right, 0, 0), DFS preorder behind a wrapper (child 0 = root).
+//          Rmax) (left, right, 0, 0), DFS preorder behind a wrapper (child 0 = root;
+//          row 3 .z = HRPP predictor id, .w = kBvh2TriOnly).
 // One HRPP table slot (32 B): a 48-bit ray hash (hrpp.rs:172-193; ~0 = empty) and
 // up to kHrppIds predicted leaf nodes (the reference keeps an unbounded set; the
 // paper's implementation, which hrpp.rs:62 cites, keeps 5).

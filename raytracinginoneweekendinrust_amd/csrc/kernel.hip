@@ -431,6 +431,11 @@ RT_DEV bool tri_t(f4 t0, f4 t1, f4 t2, const Ray& r, float tmin, float tmax, flo
 // rects or moving spheres (BVH leaf tests otherwise handle spheres, cubes, triangles).
 constexpr uint32_t kFBvh = 1u, kFTri = 2u, kFRuns = 4u, kFDeep = 8u, kFLeafRM = 16u, kFMarble = 32u, kFAll = 63u;
 // kFMarble: Marble textures, whose Perlin turbulence the whole wave evaluates together (turbulence_wave).
+// kFSusp (a strategy, not a scene feature): the suspending list walk (world_walk), for the
+// triangle-BVH preset, whose deep unpruned traversals ran at ~2 active lanes in their tails.
+// Measured on the same box (50-spp frames): C4 197 -> 128 ms; the flat / sphere-BVH presets
+// are 5-8% slower with it (C3 124 -> 133 ms, C5 152 -> 160 ms), so only that preset uses it.
+constexpr uint32_t kFSusp = 64u;
 [[maybe_unused]] constexpr uint32_t kStackLdsMax = 19u;  // LDS stack entries per lane at most (9.5 KB per wave: 16 waves/CU)
 // One leaf (primitive or cube). tmax = closest so far; a hit with t == closest is
 // accepted, so later candidates win ties exactly like hittable.rs:110-116.
@@ -584,13 +589,17 @@ RT_DEV bool bvh_hit_reference(const DevScene& S, uint32_t wrapper2, const Ray& r
                               float& closest, uint32_t& hit_code, uint32_t* stk) {
     const float tmax = closest;
     const f4* w = S.nodes2 + 4 * (size_t)wrapper2;
+    const f4 w3 = ld4(w + 3);
+    if ((__float_as_uint(w3.w) & rtdev::kBvh2TriOnly) &&
+        (r.o.x != r.o.x || r.o.y != r.o.y || r.o.z != r.o.z || r.d.x != r.d.x || r.d.y != r.d.y || r.d.z != r.d.z))
+        return false;  // no triangle takes a NaN ray (device_scene.hpp kBvh2TriOnly): the recursion's answer
     {
         f4 w0 = ld4(w), w1 = ld4(w + 1);
         float te;
         if (!slab(w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, r, inv, tmin, tmax, te)) return false;  // bvh.rs:370
     }
     uint32_t sp = 1u;
-    stk[0] = __float_as_uint(ld4(w + 3).x);
+    stk[0] = __float_as_uint(w3.x);
     stk[64] = 0u;
     bool rh = false, returning = false;
     float rt = 0.0f;
@@ -869,12 +878,49 @@ RT_DEV void sort2(float& ta, uint32_t& ca, float& tb, uint32_t& cb) {  // branch
 // to an axis plane (a zero direction component) gets t = (k - o) / d = 0 / 0 from
 // a rect whose plane holds its origin, and every comparison against NaN passes
 // (rectangle.rs:36-65); its sample is re-traced by the reference kernel.
+// A BVH traversal's state between visits (bvh_run).
+struct Trav {
+    uint32_t cur, sp, best_rank;
+    float tmax_entry;
+    bool any;
+};
+// Audit build: every completed fast traversal is replayed with the reference recursion
+// (bvh_hit_reference, on the lane's now free LDS stack); disagreements are recorded.
+RT_DEV void trav_audit(const DevScene& S, const f4* wrapper, uint32_t root, const Ray& r, V inv, float tmin,
+                       const Trav& tv, float closest, uint32_t hit_code, uint32_t* stk) {
+#ifdef RT_LEAF_AUDIT
+    const bool any = tv.any;
+    float c2 = tv.tmax_entry;
+    uint32_t h2 = 0u;
+    bool a2 = bvh_hit_reference(S, __float_as_uint(wrapper[7].z), r, to_d(r), inv, tmin, c2, h2, stk);
+    bool same = a2 == any && (!any || (__float_as_uint(c2) == __float_as_uint(closest) && h2 == hit_code));
+    if (!same) {
+        unsigned i_ = atomicAdd(&g_trav_audit_count, 1u);
+        if (i_ < kAuditMax) {
+            TravAudit& A = g_trav_audit[i_];
+            A.o[0] = r.o.x; A.o[1] = r.o.y; A.o[2] = r.o.z;
+            A.d[0] = r.d.x; A.d[1] = r.d.y; A.d[2] = r.d.z;
+            A.tmin = tmin; A.tmax = tv.tmax_entry;
+            A.fast_t = any ? closest : kInf; A.ref_t = a2 ? c2 : kInf;
+            A.fast_code = any ? hit_code : 0xffffffffu; A.ref_code = a2 ? h2 : 0xffffffffu;
+            A.root = root;
+        }
+    }
+#endif
+}
+// The suspending walk lets a traversal stop only after this many visits in one call.
+#ifndef RT_SUSP_MIN_TRIPS
+#define RT_SUSP_MIN_TRIPS 2
+#endif
+constexpr uint32_t kSuspMinTrips = RT_SUSP_MIN_TRIPS;
+template <int kKind, uint32_t kF, bool kSusp>
+RT_DEV bool bvh_run(const DevScene& S, float delta, const f4* wrapper, const Ray& r, V inv, float tmin, float& closest,
+                    uint32_t& hit_code, uint32_t* stk, uint32_t mode, Trav& tv, uint32_t susp);
 template <int kKind, uint32_t kF = kFAll>
 RT_DEV bool bvh_hit(const DevScene& S, float delta, uint32_t root, const Ray& r, float tmin, float& closest,
                     uint32_t& hit_code, uint32_t* stk, uint32_t mode, bool& replay) {
     PROF_T0(pcall);
     PROF_T0(psetup);
-    const float tmax_entry = closest;
     const f4* wrapper = S.nodes + (size_t)root * rtdev::kBvhNodeF4;
     const V inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
     if constexpr (kKind == 1 || kKind == 2) {
@@ -909,16 +955,47 @@ RT_DEV bool bvh_hit(const DevScene& S, float delta, uint32_t root, const Ray& r,
             return false;
         }
     }
+    PROF_ADD(kPrBvhSetup, psetup);
+    Trav tv{root, 0u, 0u, closest, false};
+    bvh_run<kKind, kF, false>(S, delta, wrapper, r, inv, tmin, closest, hit_code, stk, mode, tv, 0u);
+    const bool any = tv.any;
+    PROF_ADD(kPrBvhCall, pcall);
+    trav_audit(S, wrapper, root, r, inv, tmin, tv, closest, hit_code, stk);
+    return any;
+}
+
+// The fast BVH4 traversal loop from state tv: tv.cur is the next node to visit, tv.sp the
+// entries on the lane's stack, tv.tmax_entry the t_max the BVH was entered with (every box
+// test uses it), tv.best_rank / tv.any the best candidate so far (its t in `closest`, its
+// code in `hit_code`). Returns true when the traversal is complete.
+// kSusp (the suspending world walk, world_walk): before each visit, once the wave has made
+// kSuspMinTrips visits in this call and at most `susp` of its lanes are still traversing,
+// every remaining lane stops, keeps its state in tv (its stack stays in LDS) and returns
+// false; the walk resumes it on a later trip of the sample loop, together with the lanes
+// that reach the same BVH then. The visit order and every value are unchanged, only when a
+// visit runs differs, so the result is the same bits.
+template <int kKind, uint32_t kF, bool kSusp>
+RT_DEV bool bvh_run(const DevScene& S, float delta, const f4* wrapper, const Ray& r, V inv, float tmin, float& closest,
+                    uint32_t& hit_code, uint32_t* stk, uint32_t mode, Trav& tv, uint32_t susp) {
+    const float tmax_entry = tv.tmax_entry;
     const bool prune = (__float_as_uint(wrapper[7].w) & rtdev::kBvhPrunable) != 0u || (mode & kModePruneAllExp);
     const float dmi = delta * fmaxf(fmaxf(__builtin_fabsf(inv.x), __builtin_fabsf(inv.y)), __builtin_fabsf(inv.z));
     const bool leaf_boxes = prune && !(mode & kModeNoLeafBoxes);
-    bool any = false;
-    uint32_t best_rank = 0, sp = 0, cur = root;
-    PROF_ADD(kPrBvhSetup, psetup);
+    bool any = tv.any;
+    uint32_t best_rank = tv.best_rank, sp = tv.sp, cur = tv.cur;
+    bool finished = true;
+    [[maybe_unused]] uint32_t trips = 0;
 #ifdef RT_PROFILE_REGIONS
     uint32_t visits = 0;
 #endif
     for (;;) {
+        if constexpr (kSusp) {
+            if (trips >= kSuspMinTrips && (uint32_t)__popcll(__ballot(1)) <= susp) {
+                finished = false;
+                break;
+            }
+            ++trips;
+        }
         // One batch of loads per step: a leaf node needs the .xy halves of its
         // rows, an interior node its six box rows and child codes.
         const bool leaf_node = (cur & rtdev::kLeafNodeFlag) != 0u;
@@ -1068,7 +1145,7 @@ RT_DEV bool bvh_hit(const DevScene& S, float delta, uint32_t root, const Ray& r,
         PROF_ADD(kPrBvhPop, ppop);
         if (!found) break;
     }
-    PROF_ADD(kPrBvhCall, pcall);
+    tv = Trav{cur, sp, best_rank, tmax_entry, any};
 #ifdef RT_PROFILE_REGIONS
     {
         const uint32_t b = trips_bin(visits);
@@ -1085,27 +1162,7 @@ RT_DEV bool bvh_hit(const DevScene& S, float delta, uint32_t root, const Ray& r,
         if (__lane_id() == first) prof_lds[3u * kPrCount + 8u + trips_bin(m)] += 1u;
     }
 #endif
-#ifdef RT_LEAF_AUDIT
-    {  // the replay of the reference recursion must agree with the fast traversal
-        float c2 = tmax_entry;
-        uint32_t h2 = 0u;
-        bool a2 = bvh_hit_reference(S, __float_as_uint(wrapper[7].z), r, to_d(r), inv, tmin, c2, h2, stk);
-        bool same = a2 == any && (!any || (__float_as_uint(c2) == __float_as_uint(closest) && h2 == hit_code));
-        if (!same) {
-            unsigned i_ = atomicAdd(&g_trav_audit_count, 1u);
-            if (i_ < kAuditMax) {
-                TravAudit& A = g_trav_audit[i_];
-                A.o[0] = r.o.x; A.o[1] = r.o.y; A.o[2] = r.o.z;
-                A.d[0] = r.d.x; A.d[1] = r.d.y; A.d[2] = r.d.z;
-                A.tmin = tmin; A.tmax = tmax_entry;
-                A.fast_t = any ? closest : kInf; A.ref_t = a2 ? c2 : kInf;
-                A.fast_code = any ? hit_code : 0xffffffffu; A.ref_code = a2 ? h2 : 0xffffffffu;
-                A.root = root;
-            }
-        }
-    }
-#endif
-    return any;
+    return finished;
 }
 
 // Translate (instance.rs:39) / RotateY (instance.rs:104-110, 121-124) applied to a ray.
@@ -1685,6 +1742,81 @@ RT_DEV bool world_hit(const DevScene& S, float delta, const Ray& r, Rng& g, cons
     return any;
 }
 
+// The suspending list walk of the fast kernel (instances with kFSusp): hittable.rs:100-118 per lane from
+// its own position. A lane's walk state survives the trips of the sample loop: when a BVH
+// traversal is suspended (bvh_run<.., true>: at most `susp` lanes of the wave were left in
+// it), the lane stops its walk there, the others finish theirs and shade, and on the next
+// trip the suspended lanes resume that traversal together with the lanes whose new
+// segment reaches the same BVH. The long traversal tails, which ran at a few active lanes,
+// then share their visits with fresh traversals. Each lane still visits the entries in list
+// order with the same closest_so_far, and draws the medium's ln(U) where the reference does.
+struct Walk {
+    uint32_t pos;        // next entry of the segment's walk; num_top once the walk is complete
+    bool resume;         // entry `pos` is a BVH whose traversal is suspended in tv
+    bool any;            // hittable.rs:104 hit_anything
+    float closest;       // hittable.rs:106 closest_so_far
+    uint32_t hit_entry, hit_code;
+    Trav tv;
+};
+template <uint32_t kF>
+RT_DEV void world_walk(const DevScene& S, float delta, const Ray& ray, Rng& g, const Key& k, Walk& w, bool active,
+                       uint32_t* stk, uint32_t mode, bool& replay, uint32_t susp) {
+    for (uint32_t e = 0; e < S.num_top; ++e) {
+        if (!(active && w.pos == e)) continue;
+        PROF_T0(pe);
+        const DevEntry* E = S.entries + e;
+        if (E->kind == rtdev::kEntMedium) {
+            float t;
+            if (medium_hit<0, kF>(S, delta, E, ray, 0.001f, w.closest, g, k, t, stk, mode, replay)) {
+                w.closest = t;
+                w.hit_entry = e;
+                w.hit_code = rtdev::leaf_code(rtdev::kLeafMedium, 0);
+                w.any = true;
+            }
+            w.pos = e + 1u;
+        } else if ((kF & kFBvh) && E->kind == rtdev::kEntBvh) {
+            Ray r = ray;
+            const uint32_t ntf = E->ntf;
+            for (uint32_t i = 0; i < ntf; ++i) r = apply_op(E->tf[i], r);
+            const uint32_t root = E->payload;
+            const f4* wrapper = S.nodes + (size_t)root * rtdev::kBvhNodeF4;
+            const V inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
+            if (!w.resume) {  // bvh_hit's hand-over rule (NaN-prone rays go to the reference kernel)
+                const float ax = __builtin_fabsf(inv.x), ay = __builtin_fabsf(inv.y), az = __builtin_fabsf(inv.z);
+                const bool fast = ax > 0.0f && ax < kInf && ay > 0.0f && ay < kInf && az > 0.0f && az < kInf &&
+                                  __builtin_fabsf(r.o.x) < kInf && __builtin_fabsf(r.o.y) < kInf &&
+                                  __builtin_fabsf(r.o.z) < kInf;
+                if (!fast) {
+                    replay = true;
+                    w.pos = S.num_top + 1u;  // abandoned: the sample is re-traced by the reference kernel
+                    continue;
+                }
+                w.tv = Trav{root, 0u, 0u, w.closest, false};
+            }
+            if (bvh_run<0, kF, true>(S, delta, wrapper, r, inv, 0.001f, w.closest, w.hit_code, stk, mode, w.tv, susp)) {
+                trav_audit(S, wrapper, root, r, inv, 0.001f, w.tv, w.closest, w.hit_code, stk);
+                if (w.tv.any) {
+                    w.hit_entry = e;
+                    w.any = true;
+                }
+                w.pos = e + 1u;
+                w.resume = false;
+            } else {
+                w.resume = true;
+            }
+        } else {
+            uint32_t code;
+            if (entry_geom_hit<0, kF>(S, delta, E, ray, 0.001f, w.closest, code, stk, mode, replay)) {
+                w.hit_entry = e;
+                w.hit_code = code;
+                w.any = true;
+            }
+            w.pos = e + 1u;
+        }
+        PROF_ADD(e < kPrEntryLast - kPrEntry0 ? kPrEntry0 + e : kPrEntryLast, pe);
+    }
+}
+
 // Renderer::get_color's sample loop (renderer.rs:140-146) as a work pool. Each
 // lane owns one camera sample at a time; when its path ends (ray.rs:32-62) it
 // stores the sample's radiance in the HBM sample buffer and takes the next item.
@@ -1877,6 +2009,10 @@ RT_DEV bool finish_segment(const DevScene& S, const DevParams& P, const ChunkPar
 // fixup kernel re-renders the whole chunk and takes back the fast kernel's
 // segment count.
 constexpr uint32_t kReplayCap = 1u << 20;
+#ifndef RT_SUSPEND
+#define RT_SUSPEND 16
+#endif
+constexpr uint32_t kSuspLanes = RT_SUSPEND;  // suspend a BVH traversal's tail at this many lanes or fewer
 // kWaves: the waves per SIMD the register allocator must allow. 3 (<= 168 VGPRs)
 // is the default; the fast kernel also exists at 4 (<= 128 VGPRs, a few spills),
 // launched when the scene's LDS stack fits four waves per SIMD (rt_render_launch).
@@ -1933,6 +2069,64 @@ __global__ __launch_bounds__(64, kWaves) void trace_samples(DevScene Sg, DevCame
     Ray ray{};
     ItemPool pool{0u, 0u, 0u, false};
     PROF_INIT();
+    if constexpr (kKind == 0 && (kF & kFSusp) != 0u) {  // the suspending walk (world_walk)
+        Walk w{};
+        w.pos = 0u;
+        for (;;) {
+            PROF_T0(pr);
+            if (take_sample(pool, !has, C, P, Q, k, counter, list, list_n, sbuf, lane, pixel, s_local, L, T, depth, g,
+                            ray)) {
+                has = true;
+                nseg_sample = 0;
+                w.pos = 0u;
+                w.resume = false;
+            }
+            PROF_ADD(kPrRefill, pr);
+            if (__ballot(has) == 0ull) break;  // pool exhausted and every path finished
+            if (has && w.pos == 0u && !w.resume) {  // a new segment: ray.rs:43 world.hit(r, 0.001, inf)
+                nseg_sample += 1u;
+                w.closest = kInf;
+                w.any = false;
+            }
+            bool replay = false;
+            PROF_T0(pw);
+            world_walk<kF>(S, P.prune_delta, ray, g, k, w, has, stk, mode, replay, pool.exhausted ? 0u : kSuspLanes);
+            PROF_ADD(kPrWorld, pw);
+            if (has && replay) {  // hand the sample to the reference kernel
+                unsigned idx = atomicAdd(&ctr->replay_count, 1u);
+                if (idx < kReplayCap) replay_list[idx] = ReplayItem{pixel, s_local};
+                has = false;
+            }
+            const bool walked = has && w.pos == S.num_top;
+            if constexpr ((kF & kFMarble) != 0u) {
+                Rec rec;
+                rec.p = mk(0.0f, 0.0f, 0.0f);
+                uint32_t tex = 0u, tab = 0u;
+                bool marble = false;
+                if (walked && w.any) {
+                    make_record<kF>(S, w.hit_entry, w.hit_code, w.closest, ray, rec);
+                    const DevMaterial& m = S.mats[rec.mat];
+                    if (m.kind == rtdev::kMatLight || m.kind == rtdev::kMatLambertian || m.kind == rtdev::kMatIsotropic) {
+                        tex = tex_resolve(S, m.tex, rec.p);
+                        const DevTexture& tx = S.texs[tex];
+                        marble = tx.kind == rtdev::kTexMarble;
+                        tab = tx.a;
+                    }
+                }
+                const double turb = turbulence_wave(S.perm, marble, rec.p, tab);
+                if (walked &&
+                    finish_segment_rec(S, P, Q, k, sbuf, w.any, rec, tex, turb, ray, L, T, depth, g, pixel, s_local)) {
+                    has = false;
+                    nseg += nseg_sample;
+                }
+            } else if (walked && finish_segment<kF>(S, P, Q, k, sbuf, w.any, w.hit_entry, w.hit_code, w.closest, ray, L,
+                                                    T, depth, g, pixel, s_local)) {
+                has = false;
+                nseg += nseg_sample;
+            }
+            if (walked) w.pos = 0u;
+        }
+    } else
     for (;;) {
         PROF_T0(pr);
         if (take_sample(pool, !has, C, P, Q, k, counter, list, list_n, sbuf, lane, pixel, s_local, L, T, depth, g,
@@ -2230,7 +2424,7 @@ TraceKernel fast_instance(uint32_t features) {
     if ((features & ~kFRuns) == 0u) return preset_instance<kWaves, kFRuns>();
     if ((features & ~kFBvh) == 0u) return preset_instance<kWaves, kFBvh>();
     if ((features & ~(kFBvh | kFMarble)) == 0u) return preset_instance<kWaves, kFBvh | kFMarble>();
-    if ((features & ~(kFBvh | kFTri | kFDeep)) == 0u) return preset_instance<kWaves, kFBvh | kFTri | kFDeep>();
+    if ((features & ~(kFBvh | kFTri | kFDeep)) == 0u) return preset_instance<kWaves, kFBvh | kFTri | kFDeep | kFSusp>();
     return preset_instance<kWaves, kFAll>();
 }
 TraceKernel fast_instance(int waves, uint32_t features) {

@@ -811,6 +811,12 @@ class Lowerer {
         };
         const Box none2{{0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f}};
         put2(base2, tn[troot].box, none2, remap2[troot], rtdev::kChildEmpty);
+        bool tri_only = true;
+        for (const TNode& t : tn)
+            for (int k = 0; k < 2; ++k)
+                if (!t.is_node[k] && t.child[k] != rtdev::kChildEmpty && rtdev::leaf_type(t.child[k]) != rtdev::kLeafTri)
+                    tri_only = false;
+        s_->nodes2[4 * (size_t)base2 + 3].w = bitsf(tri_only ? rtdev::kBvh2TriOnly : 0u);
         for (uint32_t i = 0; i < tn.size(); ++i) {
             Box cb[2];
             uint32_t cc[2];

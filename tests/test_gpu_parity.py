@@ -163,6 +163,53 @@ def test_instances_media_and_nested_lists(rt, orc):
         np.testing.assert_array_equal(got, want)
 
 
+def _mesh_scene(rt):
+    # Triangle-BVH scene (the kFSusp preset: the suspending list walk): a lat-long sphere
+    # mesh of 1,152 triangles in a BVH under RotateY + Translate, a second BVH (spheres),
+    # a fog medium with a sphere boundary between them (its ln(U) draw must stay in list
+    # order when a lane's walk is suspended), glass, a light and a ground sphere.
+    b = rt.SceneBuilder()
+    white = b.lambertian_from_color((0.73, 0.73, 0.73))
+    red = b.lambertian_from_color((0.65, 0.05, 0.05))
+    glass = b.dielectric(1.5)
+    light = b.diffuse_light_from_color((6, 6, 6))
+    nu, nv = 32, 18
+    tris = rt.HittableList()
+    for j in range(nv):
+        for i in range(nu):
+            pts = []
+            for (a, c) in ((i, j), (i + 1, j), (i + 1, j + 1), (i, j + 1)):
+                th, ph = np.pi * c / nv, 2 * np.pi * a / nu
+                pts.append((1.5 * np.sin(th) * np.cos(ph), 1.5 * np.cos(th), 1.5 * np.sin(th) * np.sin(ph)))
+            tris.add(b.tri(pts[0], pts[1], pts[2], red if (i + j) % 5 == 0 else white))
+            tris.add(b.tri(pts[0], pts[2], pts[3], white))
+    balls = rt.HittableList()
+    for i in range(24):
+        balls.add(b.sphere((0.9 * (i % 6) - 2.5, 0.4 + 0.5 * (i // 6), -2.0 - 0.3 * (i % 2)), 0.3, white))
+    w = rt.HittableList()
+    w.add(b.sphere((0, -1000.5, 0), 1000.0, white))
+    w.add(b.bvh(balls, 0.0, 1.0, axis_seed=3))
+    w.add(b.constant_medium_from_color(b.sphere((0, 1, 0), 4.5, glass), 0.05, (0.9, 0.9, 0.95)))
+    w.add(b.translate(b.rotate_y(b.bvh(tris, 0.0, 1.0, axis_seed=11), 20.0), (0.3, 1.2, 0.5)))
+    w.add(b.sphere((2.3, 0.5, 1.5), 0.5, glass))
+    w.add(b.xz_rect(-2, 2, -2, 2, 5.5, light))
+    return b.finish(w)
+
+
+@pytest.mark.parametrize("w,h,spp", [(64, 48, 6), (9, 1, 4)])
+def test_suspending_walk_matches_oracle(w, h, spp, rt, orc):
+    # The triangle-BVH preset suspends the long tails of BVH traversals and resumes them on a
+    # later trip of the sample loop (kernel.hip world_walk): same bits and segment counts as
+    # the oracle, also for H = 1 (every ray has an infinite 1/d and goes to the reference kernel).
+    sc = _mesh_scene(rt)
+    cam = rt.Camera.new((0, 2, 9), (0, 1, 0), (0, 1, 0), 40.0, w / h, 0.05, 9.0, 0.0, 1.0)
+    params = rt.render_params(w, h, spp, 16, background=(0.05, 0.05, 0.08), seed=7)
+    want, cnt = orc.render(sc, cam, params)
+    got, st = gpu_render(rt, sc, cam, params)
+    np.testing.assert_array_equal(got, want)
+    assert st["segments"] == cnt["segments"]
+
+
 # --- sharding / determinism (the multi-GPU decomposition) ---------------------------
 @pytest.mark.parametrize("n", [2, 3, 8])
 def test_gpu_shards_compose_bit_identically(n, rt):
@@ -216,7 +263,7 @@ def test_full_workload_subsample_matches_oracle(cfg_name, shard, rt, orc):
     assert np.isfinite(got).all()
 
 
-@pytest.mark.parametrize("cfg_name,spp", [("C3", 500), ("C2", 8), ("C1", 16)])
+@pytest.mark.parametrize("cfg_name,spp", [("C3", 500), ("C2", 8), ("C1", 16), ("C4", 100)])
 def test_pruned_traversal_equals_reference_traversal_full_frame(cfg_name, spp, rt):
     # Closest-hit box pruning and leaf-box rejects must not change a single path:
     # same bits AND the same number of ray segments as the reference's unpruned
@@ -236,19 +283,21 @@ def test_pruned_traversal_equals_reference_traversal_full_frame(cfg_name, spp, r
     assert out[True][1]["segments"] == out[False][1]["segments"]
 
 
-def test_traversal_audit_full_c3_frame():
-    # The audit build replays EVERY fast BVH traversal of a full C3 frame (500 spp)
-    # with the literal bvh.rs recursion and re-tests every leaf-box reject; both
-    # counts must be 0. Per-call (t, primitive) equality is stricter than the image
-    # tests: a tie resolved to the wrong coplanar face can shade identically.
+@pytest.mark.parametrize("cfg_name,spp", [("C3", 500), ("C4", 100)])
+def test_traversal_audit_full_frame(cfg_name, spp):
+    # The audit build replays EVERY fast BVH traversal of a full C3 frame (500 spp) and of
+    # a full-resolution C4 frame (the suspending walk over the triangle BVH) with the
+    # literal bvh.rs recursion and re-tests every leaf-box reject; both counts must be 0.
+    # Per-call (t, primitive) equality is stricter than the image tests: a tie resolved
+    # to the wrong coplanar face can shade identically.
     import subprocess
     import sys
     root = os.path.dirname(HERE)
     lib = os.path.join(root, "raytracinginoneweekendinrust_amd", "_lib", "librtamd_audit.so")
     assert os.path.exists(lib), "build() makes the audit library"
     env = dict(os.environ, RT_LIBRARY=lib)
-    r = subprocess.run([sys.executable, os.path.join(root, "tools", "region_profile.py"), "--config", "C3",
-                        "--spp", "500"], capture_output=True, text=True, env=env, timeout=600)
+    r = subprocess.run([sys.executable, os.path.join(root, "tools", "region_profile.py"), "--config", cfg_name,
+                        "--spp", str(spp)], capture_output=True, text=True, env=env, timeout=600)
     assert r.returncode == 0, r.stderr[-2000:]
     out = r.stdout + r.stderr
     assert '{"leaf_audit_count": 0}' in out, out[-2000:]
