@@ -204,7 +204,13 @@ RT_DEV void philox(uint32_t& c0, uint32_t& c1, uint32_t& c2, uint32_t& c3, uint3
 struct Key {
     uint32_t k0, k1;
 };
-__device__ __noinline__ uint4 philox_block(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t k0, uint32_t k1) {
+
+#ifdef RT_PHILOX_INLINE
+__device__ __forceinline__
+#else
+__device__ __noinline__
+#endif
+uint4 philox_block(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t k0, uint32_t k1) {
     uint32_t c3 = 0u;
     philox(c0, c1, c2, c3, k0, k1);
     return make_uint4(c0, c1, c2, c3);
@@ -2306,7 +2312,7 @@ __global__ void kat_eval(int op, const float* __restrict__ in, float* __restrict
 
 }  // namespace
 
-#ifdef RT_INSTANCES_TU
+#if defined(RT_INSTANCES_TU) && RT_INSTANCES_TU == 1
 // kernel_mc.hip: this translation unit holds only the 4-wave instances of the
 // BVH-only and the sphere-run presets, built with the memory-clause scheduler.
 void* rt_mc_trace_instance(uint32_t preset) {
@@ -2315,9 +2321,16 @@ void* rt_mc_trace_instance(uint32_t preset) {
     if (preset == kFRuns) return reinterpret_cast<void*>(trace_samples<0, 4, kFRuns>);
     return nullptr;
 }
+#elif defined(RT_INSTANCES_TU) && RT_INSTANCES_TU == 2
+// kernel_flat.hip: the flat-list preset (no BVH, no long sphere runs: C5) with
+// philox_block inlined (RT_PHILOX_INLINE).
+void* rt_flat_trace_instance(int waves) {
+    return waves == 4 ? reinterpret_cast<void*>(trace_samples<0, 4, 0u>) : reinterpret_cast<void*>(trace_samples<0, 3, 0u>);
+}
 #else
 #ifdef RT_SPLIT_MC
 void* rt_mc_trace_instance(uint32_t preset);  // kernel_mc.hip
+void* rt_flat_trace_instance(int waves);      // kernel_flat.hip
 #endif
 
 // ===========================================================================
@@ -2409,14 +2422,25 @@ using TraceKernel = void (*)(DevScene, DevCamera, DevParams, ChunkParams, float*
 // come from kernel_mc.hip, compiled with the memory-clause scheduling strategy:
 // measured on the same box it is 1.3% faster on C3 and 1.2% on C2 but 1-2% slower
 // on the other presets (C4, C5), and a scheduling strategy is a per-file flag.
+// Diagnostic builds only (-DRT_SUSP_ALL, A/B of the suspending walk on every preset).
+#ifdef RT_SUSP_ALL
+constexpr uint32_t kSuspAll = kFSusp;
+#else
+constexpr uint32_t kSuspAll = 0u;
+#endif
+// The flat-list instances come from kernel_flat.hip, where philox_block is inlined: the
+// call's register saves cost that preset 8% (C5 151 -> 140 ms per 200-spp frame, same box),
+// while the BVH presets are 1-2% slower with it inlined (C3, C4) and C2 is unchanged.
 template <int kWaves, uint32_t kF>
 TraceKernel preset_instance() {
 #ifdef RT_SPLIT_MC
-    if constexpr (kWaves == 4 && (kF == kFBvh || kF == (kFBvh | kFMarble) || kF == kFRuns))
+    if constexpr (kSuspAll == 0u && kWaves == 4 && (kF == kFBvh || kF == (kFBvh | kFMarble) || kF == kFRuns))
         return reinterpret_cast<TraceKernel>(rt_mc_trace_instance(kF));
+    else if constexpr (kSuspAll == 0u && kF == 0u)
+        return reinterpret_cast<TraceKernel>(rt_flat_trace_instance(kWaves));
     else
 #endif
-        return trace_samples<0, kWaves, kF>;
+        return trace_samples<0, kWaves, kF | kSuspAll>;
 }
 template <int kWaves>
 TraceKernel fast_instance(uint32_t features) {

@@ -1,0 +1,7 @@
+// The trace_samples instances of the flat-list preset (no BVH, no long sphere runs:
+// C5), compiled from kernel.hip with philox_block inlined (RT_PHILOX_INLINE): the
+// out-of-line call's register saves cost that preset 8%. kernel.hip's fast_instance
+// launches them through rt_flat_trace_instance.
+#define RT_INSTANCES_TU 2
+#define RT_PHILOX_INLINE 1
+#include "kernel.hip"
