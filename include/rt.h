@@ -258,9 +258,36 @@ int rt_format_ppm(const float* d_rgb, uint32_t width, uint32_t height, char* d_t
  * to d_order the item indices in the order the reference recursion leaves them
  * (random axis per node, stable total_cmp sort, split at n / 2, two-item nodes
  * ordered by one comparison). Synchronises `stream`. rt_scene_upload uses it for
- * BVHs of >= 16384 items (RT_BVH_BUILD=host|device|auto overrides: "device" builds
- * every BVH on the device, "host" none); the lowered tree is identical either way. */
+ * BVHs of >= 16384 items (RT_OPT_BVH_BUILD overrides: "device always" builds every
+ * BVH on the device, "host always" none); the lowered tree is identical either way. */
 int rt_bvh_build_order(const float* d_keys, uint32_t n, uint64_t seed, uint32_t* d_order, void* stream);
+
+/* Diagnostic options (tests, A/B runs, experiments). The library reads no environment
+ * variables: each switch below is process-wide, starts at its default, and changes only
+ * through rt_set_option. None is needed for production renders.
+ *   RT_OPT_TUNE             traversal mode bits (kernel.hip kMode*; default 0). Bit 16 sends
+ *                           the replay pass through the literal reference kernel.
+ *   RT_OPT_GROUP            samples per batch (1..64; 0 = automatic, the default)
+ *   RT_OPT_STACK_LDS        cap on the LDS part of the traversal stack, read at upload
+ *                           (>= 1; 0 = the default 19 entries); deeper stacks spill to HBM
+ *   RT_OPT_SAMPLE_BUFFER_MB sample-buffer budget in MiB (0 = 40% of free HBM, the default)
+ *   RT_OPT_HRPP_SLOT_BITS   log2 HRPP table slots per predictor (-1 = 22, the default; 0..28)
+ *   RT_OPT_LAUNCH_LOG       1 = print the launched kernel instance and replay counts on stderr
+ *   RT_OPT_BVH_BUILD        leaf ordering of BVHs at upload: 0 = device for >= 16384 items
+ *                           (default), 1 = host always, 2 = device always
+ * Returns RT_ERR_INVALID for an unknown option or a value out of range. */
+typedef enum {
+    RT_OPT_TUNE = 0,
+    RT_OPT_GROUP = 1,
+    RT_OPT_STACK_LDS = 2,
+    RT_OPT_SAMPLE_BUFFER_MB = 3,
+    RT_OPT_HRPP_SLOT_BITS = 4,
+    RT_OPT_LAUNCH_LOG = 5,
+    RT_OPT_BVH_BUILD = 6,
+    RT_OPT_COUNT = 7
+} rt_option;
+int rt_set_option(int option, int64_t value);
+int rt_get_option(int option, int64_t* value);
 
 /* HRPP statistics of the last RT_FLAG_HRPP render (src/hrpp.rs:91-127): for
  * predictor p (in lowering order) out[6 p + 0..5] = true-positive, false-positive

@@ -27,6 +27,10 @@ RT_FLAG_HRPP = 2
 RT_FLAG_ACCUMULATE = 4
 RT_FLAG_RAW_SUM = 8
 
+# rt_option (rt_set_option): the library's diagnostic switches; it reads no environment
+OPTIONS = {"tune": 0, "group": 1, "stack_lds": 2, "sample_buffer_mb": 3, "hrpp_slot_bits": 4, "launch_log": 5,
+           "bvh_build": 6}
+
 STATUS = {0: "RT_OK", -1: "RT_ERR_INVALID", -2: "RT_ERR_UNSUPPORTED", -3: "RT_ERR_HIP", -4: "RT_ERR_OOM",
           -5: "RT_ERR_NO_DEVICE", -6: "RT_ERR_IO"}
 
@@ -121,6 +125,8 @@ SIGNATURES = [
     ("rt_shard_pack", C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p]),
     ("rt_shard_unpack", C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p]),
     ("rt_device_kat", C.c_int, [C.c_int, C.POINTER(C.c_float), C.POINTER(C.c_float), C.c_uint32]),
+    ("rt_set_option", C.c_int, [C.c_int, C.c_int64]),
+    ("rt_get_option", C.c_int, [C.c_int, C.POINTER(C.c_int64)]),
 ]
 
 

@@ -152,11 +152,13 @@ struct DevScene {
     const uint32_t* hrpp_vals;            // -> wrapper-format record of the leaf node
     unsigned long long* hrpp_stats;       // per predictor: tp, fp, np, dropped
     uint32_t* hrpp_cnt;                   // per-wave LDS counters (set in the kernel)
-    uint32_t hrpp_bits, hrpp_nkeys, hrpp_npred, pad0;
+    uint32_t hrpp_bits, hrpp_nkeys, hrpp_npred;
+    uint32_t num_nodes2;  // BVH2 records (the audit build bounds-checks every visited index)
     // Deep BVHs (instances with kFDeep): stack entries past stack_depth live in HBM,
     // stack_spill[((wave * spill_depth + entry - stack_depth) * 64 + lane) * 2 + {node, t}]
     uint32_t* stack_spill;
-    uint32_t spill_depth, pad1;
+    uint32_t spill_depth;
+    uint32_t num_nodes;   // BVH4 nodes (the audit build bounds-checks every visited index)
 };
 
 // Camera::new (camera.rs:44-81) evaluated on the host.

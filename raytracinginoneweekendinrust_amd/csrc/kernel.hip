@@ -25,6 +25,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <atomic>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -63,14 +64,14 @@ enum ProfRegion : uint32_t {
     kPrBvhPop = 48, kPrBvhCall = 49, kPrCount = 52
 };
 // traversal mode bits (bvh_hit): kModeExact = RT_FLAG_EXACT_BVH; the rest come
-// from DevParams::tune (RT_TUNE environment variable, diagnostics / A-B runs).
+// from DevParams::tune (rt_set_option(RT_OPT_TUNE), diagnostics / A-B runs).
 constexpr uint32_t kModeExact = 1u, kModeNoLeafBoxes = 2u, kModeNoPermLds = 32u, kModeW3 = 64u,
                    kModeNoPretest = 128u, kModeReplayRef = 1u << 16;  // ReplayRef: the replay pass runs trace_samples<1>
-// EXPERIMENT ONLY (RT_TUNE, not exact): closest-hit pruning also on BVHs the proof does not
+// EXPERIMENT ONLY (RT_OPT_TUNE, not exact): closest-hit pruning also on BVHs the proof does not
 // cover (triangles, moving spheres), to measure what an exact bound for them could gain.
 constexpr uint32_t kModePruneAllExp = 1u << 20;
 #ifdef RT_ABLATE
-// Ablation build (librtamd_ablate.so, diagnostics only): RT_TUNE bits that run a
+// Ablation build (librtamd_ablate.so, diagnostics only): RT_OPT_TUNE bits that run a
 // piece of work twice (results of the copy discarded through an opaque test),
 // so the time delta prices that work without changing any path.
 constexpr uint32_t kAbLeaf2 = 1u << 8, kAbKeys2 = 1u << 9, kAbBvh2 = 1u << 10, kAbMedium2 = 1u << 11,
@@ -133,6 +134,10 @@ struct TravAudit {
     uint32_t fast_code, ref_code, root;
 };
 __device__ unsigned g_trav_audit_count;
+// and every visited / pushed BVH node index and stack position is bounds-checked: a
+// violation (e.g. a non-finite slab value steering the traversal) is counted and the
+// traversal stops instead of faulting
+__device__ unsigned g_bounds_audit_count;
 __device__ TravAudit g_trav_audit[kAuditMax];
 #endif
 
@@ -631,6 +636,12 @@ RT_DEV bool bvh_hit_reference(const DevScene& S, uint32_t wrapper2, const Ray& r
             if (sp == 0u) break;
             continue;
         }
+#ifdef RT_LEAF_AUDIT
+        if (F[0] >= S.num_nodes2 || 2u * sp > S.stack_depth) {  // a frame is two 128-word stack entries
+            atomicAdd(&g_bounds_audit_count, 1u);
+            break;
+        }
+#endif
         const f4* nd = S.nodes2 + 4 * (size_t)F[0];
         f4 n0 = ld4(nd), n1 = ld4(nd + 1), n2 = ld4(nd + 2), n3 = ld4(nd + 3);
         const uint32_t lc = __float_as_uint(n3.x), rc = __float_as_uint(n3.y);
@@ -884,6 +895,7 @@ RT_DEV void sort2(float& ta, uint32_t& ca, float& tb, uint32_t& cb) {  // branch
 // to an axis plane (a zero direction component) gets t = (k - o) / d = 0 / 0 from
 // a rect whose plane holds its origin, and every comparison against NaN passes
 // (rectangle.rs:36-65); its sample is re-traced by the reference kernel.
+[[maybe_unused]] constexpr uint32_t kDeferBit = 0x20000000u;  // a deferred leaf node on the stack (RT_LEAF_DEFER)
 // A BVH traversal's state between visits (bvh_run).
 struct Trav {
     uint32_t cur, sp, best_rank;
@@ -1004,8 +1016,36 @@ RT_DEV bool bvh_run(const DevScene& S, float delta, const f4* wrapper, const Ray
         }
         // One batch of loads per step: a leaf node needs the .xy halves of its
         // rows, an interior node its six box rows and child codes.
+#ifdef RT_LEAF_DEFER
+        // Leaf deferral: a lane about to test a leaf node while fewer than RT_LEAF_DEFER
+        // lanes of the wave are at one (and some are at interior nodes) swaps that node
+        // with its stack top and visits the top entry now; the leaf node, marked
+        // kDeferBit, is tested when popped (never deferred twice, never pop-pruned), so
+        // leaf tests run with more lanes. Visiting a node the pop-time prune would skip
+        // only costs time: every child test is still the reference's.
+        {
+            const bool at_leaf = (cur & (rtdev::kLeafNodeFlag | kDeferBit)) == rtdev::kLeafNodeFlag;
+            const uint32_t nl = (uint32_t)__popcll(__ballot(at_leaf)), na = (uint32_t)__popcll(__ballot(1));
+            if (at_leaf && nl < (uint32_t)RT_LEAF_DEFER && nl < na && sp > 0u &&
+                (!(kF & kFDeep) || sp <= S.stack_depth)) {
+                const uint32_t x = stk[(sp - 1u) * 128u];
+                stk[(sp - 1u) * 128u] = cur | kDeferBit;
+                stk[(sp - 1u) * 128u + 64u] = __float_as_uint(-kInf);
+                cur = x;
+            }
+        }
+        const bool leaf_node = (cur & rtdev::kLeafNodeFlag) != 0u;
+        const f4* nd = S.nodes + (size_t)(cur & ~(rtdev::kLeafNodeFlag | kDeferBit)) * rtdev::kBvhNodeF4;
+#else
         const bool leaf_node = (cur & rtdev::kLeafNodeFlag) != 0u;
         const f4* nd = S.nodes + (size_t)(cur & ~rtdev::kLeafNodeFlag) * rtdev::kBvhNodeF4;
+#endif
+#ifdef RT_LEAF_AUDIT
+        if ((cur & ~(rtdev::kLeafNodeFlag | kDeferBit)) >= S.num_nodes || sp > S.stack_depth + S.spill_depth) {
+            atomicAdd(&g_bounds_audit_count, 1u);
+            break;
+        }
+#endif
 #ifdef RT_PROFILE_REGIONS
         ++visits;
 #endif
@@ -2455,6 +2495,10 @@ TraceKernel fast_instance(int waves, uint32_t features) {
     return waves == 4 ? fast_instance<4>(features) : fast_instance<3>(features);
 }
 
+// rt_set_option's process-wide diagnostic switches (include/rt.h rt_option).
+std::atomic<int64_t> g_opt[RT_OPT_COUNT] = {{0}, {0}, {0}, {0}, {-1}, {0}, {0}};
+int64_t opt(int o) { return g_opt[o].load(std::memory_order_relaxed); }
+
 int check_device(int device) {
     int n = 0;
     hipError_t e = hipGetDeviceCount(&n);
@@ -2499,12 +2543,12 @@ int rt_scene_upload(const rt_scene_desc* desc, int device, rt_scene_handle* out)
     *out = nullptr;
     rthost::HostScene hs;
     std::string err;
-    // Large BVHs are ordered on the target device (bvh_build.hip); RT_BVH_BUILD=host|device|auto.
-    const char* mode = getenv("RT_BVH_BUILD");
+    // Large BVHs are ordered on the target device (bvh_build.hip); RT_OPT_BVH_BUILD overrides.
+    const int64_t mode = opt(RT_OPT_BVH_BUILD);
     int dev = device;
     rthost::BvhOrderer orderer{16384u, rthost::device_bvh_order, &dev};
-    if (mode && !strcmp(mode, "device")) orderer.min_items = 1u;
-    const bool host_only = mode && !strcmp(mode, "host");
+    if (mode == 2) orderer.min_items = 1u;
+    const bool host_only = mode == 1;
     int rc = rthost::lower_scene(desc, &hs, &err, host_only ? nullptr : &orderer);
     if (rc) return rthost::set_error(rc, err);
     if (hs.max_stack > 96 || hs.max_stack_ref > 96)
@@ -2574,6 +2618,8 @@ int rt_scene_upload(const rt_scene_desc* desc, int device, rt_scene_handle* out)
     d.perm = base + parts[9].off;
     d.texels = base + parts[10].off;
     d.nodes2 = (const f4*)(base + parts[11].off);
+    d.num_nodes = (uint32_t)(hs.nodes.size() / rtdev::kBvhNodeF4);
+    d.num_nodes2 = (uint32_t)(hs.nodes2.size() / 4);
     d.num_top = hs.num_top;
     d.num_entries = (uint32_t)hs.entries.size();
     d.stack_depth = hs.max_stack;
@@ -2597,8 +2643,8 @@ int rt_scene_upload(const rt_scene_desc* desc, int device, rt_scene_handle* out)
 #ifndef RT_LEAF_AUDIT  // (the audit build replays traversals on the same LDS stack: no spill area)
     {  // deep BVHs: the LDS stack keeps kStackLdsMax entries, HBM the rest
         uint32_t cap = kStackLdsMax;
-        if (const char* env = getenv("RT_STACK_LDS"))  // diagnostics / tests: a smaller LDS part (>= 1)
-            cap = std::max(1u, std::min(cap, (uint32_t)strtoul(env, nullptr, 10)));
+        if (const int64_t v = opt(RT_OPT_STACK_LDS))  // diagnostics / tests: a smaller LDS part (>= 1)
+            cap = std::min(cap, (uint32_t)v);
         if (hs.max_stack > cap) {
             s->features |= kFDeep;
             d.stack_depth = cap;
@@ -2666,6 +2712,8 @@ int rt_scene_free(rt_scene_handle s) {
                         ta[i].o[0], ta[i].o[1], ta[i].o[2], ta[i].d[0], ta[i].d[1], ta[i].d[2], ta[i].tmin, ta[i].tmax,
                         ta[i].fast_t, ta[i].ref_t, ta[i].fast_code, ta[i].ref_code, ta[i].root);
         }
+        if (hipMemcpyFromSymbol(&na, HIP_SYMBOL(g_bounds_audit_count), sizeof na) == hipSuccess)
+            fprintf(stderr, "{\"bounds_audit_count\": %u}\n", na);
 #endif
         if (s->done) (void)hipEventSynchronize(s->done);  // the last launch may still use the buffers below
         if (s->pool) (void)hipFree(s->pool);
@@ -2773,10 +2821,7 @@ int rt_render_launch_camera(rt_scene_handle s, const rt_camera* camera, const rt
     dp.num_blocks = dp.blocks_x * ((p->height + 7u) / 8u);
     dp.flags = p->flags;
     dp.spp_div = p->spp_total ? p->spp_total : p->samples_per_pixel;
-    {
-        const char* tune = getenv("RT_TUNE");  // diagnostic traversal switches (kMode* bits), default 0
-        dp.tune = tune ? (uint32_t)strtoul(tune, nullptr, 0) & ~kModeExact : 0u;
-    }
+    dp.tune = (uint32_t)opt(RT_OPT_TUNE) & ~kModeExact;  // diagnostic traversal switches (kMode* bits)
     dp.bg[0] = p->background[0];
     dp.bg[1] = p->background[1];
     dp.bg[2] = p->background[2];
@@ -2818,7 +2863,7 @@ int rt_render_launch_camera(rt_scene_handle s, const rt_camera* camera, const rt
             if (avail > budget) budget = avail;
         }
     }
-    if (const char* env = getenv("RT_SAMPLE_BUFFER_MB")) budget = strtoull(env, nullptr, 10) << 20;
+    if (const int64_t mb = opt(RT_OPT_SAMPLE_BUFFER_MB)) budget = (uint64_t)mb << 20;
     uint64_t max_s = budget / per_sample;
     if (max_s < 1) max_s = 1;
     uint32_t nchunks = (uint32_t)((p->samples_per_pixel + max_s - 1) / max_s);
@@ -2861,9 +2906,8 @@ int rt_render_launch_camera(rt_scene_handle s, const rt_camera* camera, const rt
     size_t lds_ref = (size_t)dev_ref.stack_depth * 128u * sizeof(uint32_t) + perm_lds;
     if ((dp.flags & RT_FLAG_HRPP) && s->dev.hrpp_npred) {  // the experiment: reference kernel + predictors
         dp.flags |= RT_FLAG_EXACT_BVH;
-        uint32_t bits = 22u;  // 4 M slots (128 MiB) per predictor
-        if (const char* env = getenv("RT_HRPP_SLOT_BITS")) bits = (uint32_t)strtoul(env, nullptr, 10);
-        if (bits > 28u) bits = 28u;
+        const int64_t ob = opt(RT_OPT_HRPP_SLOT_BITS);
+        const uint32_t bits = ob < 0 ? 22u : (uint32_t)ob;  // default 4 M slots (128 MiB) per predictor
         const uint64_t bytes = bits ? ((uint64_t)s->dev.hrpp_npred << bits) * sizeof(rtdev::HrppSlot) : 0u;
         if (s->hrpp_tab_bytes < bytes || !s->hrpp_stats) {
             if (s->hrpp_tab) (void)hipFree(s->hrpp_tab);
@@ -2905,7 +2949,7 @@ int rt_render_launch_camera(rt_scene_handle s, const rt_camera* camera, const rt
             }
             s->dev.stack_spill = s->stack_spill;
         }
-        if (getenv("RT_LAUNCH_LOG"))
+        if (opt(RT_OPT_LAUNCH_LOG))
             fprintf(stderr, "rt: trace_samples<0, %d, features 0x%x>: %d waves/CU (LDS %zu B/wave), reference kernel %d "
                     "waves/CU\n", s->fast_waves, s->features, per_cu, lds, per_cu_ref);
     }
@@ -2916,8 +2960,7 @@ int rt_render_launch_camera(rt_scene_handle s, const rt_camera* camera, const rt
         q.sample0 = p->sample_base + c * chunk;
         q.samples = c + 1 < nchunks ? chunk : p->samples_per_pixel - c * chunk;
         q.group = batch_group(q.samples);
-        if (const char* env = getenv("RT_GROUP"))  // diagnostics / A-B runs: samples per batch (1..64)
-            q.group = std::max(1u, std::min(64u, (uint32_t)strtoul(env, nullptr, 10)));
+        if (const int64_t gr = opt(RT_OPT_GROUP)) q.group = (uint32_t)gr;  // diagnostics / A-B runs
         q.groups_per_block = (q.samples + q.group - 1) / q.group;
         q.num_batches = nblk * q.groups_per_block;
         q.npix = (uint32_t)npix;
@@ -2959,7 +3002,7 @@ int rt_render_launch_camera(rt_scene_handle s, const rt_camera* camera, const rt
             }
         }
         if ((e = hipGetLastError()) != hipSuccess) return hip_fail(e, "trace_samples launch");
-        if (getenv("RT_LAUNCH_LOG")) {  // diagnostics: samples the fast kernel handed to the reference kernel
+        if (opt(RT_OPT_LAUNCH_LOG)) {  // diagnostics: samples the fast kernel handed to the reference kernel
             TraceCounters h{};
             if (hipMemcpyAsync(&h, s->counter, sizeof h, hipMemcpyDeviceToHost, st) == hipSuccess &&
                 hipStreamSynchronize(st) == hipSuccess)
@@ -3145,6 +3188,31 @@ int rt_render_multi_camera(rt_scene_handle* scenes, uint32_t n, const rt_camera*
         stats->kernel_ms = ms_max;
     }
     cleanup();
+    return RT_OK;
+}
+
+int rt_set_option(int option, int64_t value) {
+    rthost::clear_error();
+    if (option < 0 || option >= RT_OPT_COUNT) return rthost::set_error(RT_ERR_INVALID, "unknown option");
+    bool ok = true;
+    switch (option) {
+        case RT_OPT_TUNE: ok = value >= 0 && value <= 0xffffffffll; break;
+        case RT_OPT_GROUP: ok = value >= 0 && value <= 64; break;
+        case RT_OPT_STACK_LDS: ok = value >= 0 && value <= 96; break;
+        case RT_OPT_SAMPLE_BUFFER_MB: ok = value >= 0 && value <= (1ll << 30); break;
+        case RT_OPT_HRPP_SLOT_BITS: ok = value >= -1 && value <= 28; break;
+        case RT_OPT_LAUNCH_LOG: ok = value == 0 || value == 1; break;
+        case RT_OPT_BVH_BUILD: ok = value >= 0 && value <= 2; break;
+    }
+    if (!ok) return rthost::set_error(RT_ERR_INVALID, "option value out of range");
+    g_opt[option].store(value, std::memory_order_relaxed);
+    return RT_OK;
+}
+
+int rt_get_option(int option, int64_t* value) {
+    rthost::clear_error();
+    if (option < 0 || option >= RT_OPT_COUNT || !value) return rthost::set_error(RT_ERR_INVALID, "unknown option");
+    *value = opt(option);
     return RT_OK;
 }
 

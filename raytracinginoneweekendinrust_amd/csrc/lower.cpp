@@ -828,7 +828,7 @@ class Lowerer {
         }
         uint32_t base = (uint32_t)(s_->nodes.size() / rtdev::kBvhNodeF4);
         uint32_t total = base + 1 + (uint32_t)wide.size();
-        if (total >= rtdev::kLeafNodeFlag) return fail(RT_ERR_UNSUPPORTED, "too many BVH nodes");
+        if (total >= (rtdev::kLeafNodeFlag >> 1)) return fail(RT_ERR_UNSUPPORTED, "too many BVH nodes");
         s_->nodes.resize((size_t)total * rtdev::kBvhNodeF4);
         auto leaf_node = [&](uint32_t w) {
             for (const Slot& c : wide[w])

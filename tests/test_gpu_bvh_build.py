@@ -62,18 +62,11 @@ def test_order_one_million_items(rt):
 
 
 def render_with(rt, mode, scene, cfg, params):
-    old = os.environ.get("RT_BVH_BUILD")
-    os.environ["RT_BVH_BUILD"] = mode
-    try:
+    with rt.options(bvh_build={"auto": 0, "host": 1, "device": 2}[mode]):
         ds = rt.DeviceScene(scene)
         info = ds.info()
         img, st = ds.render(cfg.camera(), params)
         ds.close()
-    finally:
-        if old is None:
-            os.environ.pop("RT_BVH_BUILD")
-        else:
-            os.environ["RT_BVH_BUILD"] = old
     return img, st, info
 
 

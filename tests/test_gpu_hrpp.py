@@ -4,7 +4,7 @@ HRPP is approximate and its tables fill concurrently, so it has no bit-exact
 oracle (nor does the reference: bvh.rs:146-149). What is pinned here:
 * the ray hash's float mapping, bit for bit against a restatement of
   hrpp.rs:136-170 (BitPrecision::Six);
-* with no table (RT_HRPP_SLOT_BITS=0) every call is a "no prediction" and the
+* with no table (rt_set_option(RT_OPT_HRPP_SLOT_BITS, 0)) every call is a "no prediction" and the
   render is bit-identical to the exact path — the predictor plumbing changes
   nothing by itself;
 * scenes without Bvh::with_predictor are untouched by the flag;
@@ -47,20 +47,12 @@ def c3(rt, width, spp):
 
 
 def render(rt, scene, cfg, bits=None, **kw):
-    old = os.environ.get("RT_HRPP_SLOT_BITS")
-    if bits is not None:
-        os.environ["RT_HRPP_SLOT_BITS"] = str(bits)
-    try:
+    with rt.options(**({} if bits is None else {"hrpp_slot_bits": bits})):
         ds = rt.DeviceScene(scene)
         p = rt.render_params(cfg.width, cfg.height, cfg.spp, cfg.depth, background=cfg.background(), **kw)
         img, st = ds.render(cfg.camera(), p)
         stats = ds.hrpp_stats()
         ds.close()
-    finally:
-        if old is None:
-            os.environ.pop("RT_HRPP_SLOT_BITS", None)
-        else:
-            os.environ["RT_HRPP_SLOT_BITS"] = old
     return img, st, stats
 
 

@@ -302,6 +302,7 @@ def test_traversal_audit_full_frame(cfg_name, spp):
     out = r.stdout + r.stderr
     assert '{"leaf_audit_count": 0}' in out, out[-2000:]
     assert '{"trav_audit_count": 0}' in out, out[-2000:]
+    assert '{"bounds_audit_count": 0}' in out, out[-2000:]  # every visited node index and stack slot in range
 
 
 def test_sphere_pretest_audit_c2():
@@ -347,26 +348,24 @@ def test_every_feature_preset_instance(with_tri, rt, orc):
 
 
 @pytest.mark.parametrize("cfg_name", ["C3", "C4"])
-def test_stack_spill_to_hbm_matches_oracle(cfg_name, rt, orc, monkeypatch):
+def test_stack_spill_to_hbm_matches_oracle(cfg_name, rt, orc):
     # Deep BVHs keep kStackLdsMax stack entries in LDS and the rest in HBM; a 2-entry
-    # LDS part (RT_STACK_LDS, read at upload) sends almost every traversal through
+    # LDS part (rt_set_option(RT_OPT_STACK_LDS), read at upload) sends almost every traversal through
     # the HBM half, on the pruned (C3) and the unpruned triangle (C4) traversal.
-    monkeypatch.setenv("RT_STACK_LDS", "2")
     cfg, scene, params = setup(rt, cfg_name, 40, 2, seed=3)
     want, cnt = orc.render(scene, cfg.camera(), params)
-    got, st = gpu_render(rt, scene, cfg.camera(), params)
+    with rt.options(stack_lds=2):
+        got, st = gpu_render(rt, scene, cfg.camera(), params)
     np.testing.assert_array_equal(got, want)
     assert st["segments"] == cnt["segments"]
 
 
 @pytest.mark.parametrize("replay_ref", [False, True])
 @pytest.mark.parametrize("cfg_name,w,h", [("C3", 40, None), ("C5", 41, None), ("C3", 7, 1)])
-def test_replay_pass_kernels_match_oracle(cfg_name, w, h, replay_ref, rt, orc, monkeypatch):
+def test_replay_pass_kernels_match_oracle(cfg_name, w, h, replay_ref, rt, orc):
     # Samples the fast kernel hands over (rays with a zero / non-finite 1/d component) are
     # re-traced by trace_samples<3> (fast traversal except for those rays), or with
-    # RT_TUNE bit 16 by the literal replay trace_samples<1>. H = 1 makes every ray such a ray.
-    if replay_ref:
-        monkeypatch.setenv("RT_TUNE", str(1 << 16))
+    # RT_OPT_TUNE bit 16 by the literal replay trace_samples<1>. H = 1 makes every ray such a ray.
     cfg, scene, params = setup(rt, cfg_name, w, 3, seed=5)
     cam = cfg.camera()
     if h is not None:
@@ -374,6 +373,7 @@ def test_replay_pass_kernels_match_oracle(cfg_name, w, h, replay_ref, rt, orc, m
                             cfg.focus_dist, cfg.time0, cfg.time1)
         params = rt.render_params(w, h, 3, cfg.depth, background=cfg.background(), seed=5)
     want, cnt = orc.render(scene, cam, params)
-    got, st = gpu_render(rt, scene, cam, params)
+    with rt.options(tune=(1 << 16) if replay_ref else 0):
+        got, st = gpu_render(rt, scene, cam, params)
     np.testing.assert_array_equal(got, want)
     assert st["segments"] == cnt["segments"]

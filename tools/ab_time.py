@@ -25,6 +25,9 @@ from raytracinginoneweekendinrust_amd.configs import CONFIGS  # noqa: E402
 
 def bind(path):
     lib = C.CDLL(path)
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import rtopts
+    rtopts.apply_lib(lib)
     lib.rt_scene_generate.argtypes = [C.c_char_p, C.c_uint64, C.c_char_p, C.POINTER(C.POINTER(_capi.rt_scene_desc))]
     lib.rt_scene_upload.argtypes = [C.POINTER(_capi.rt_scene_desc), C.c_int, C.POINTER(C.c_void_p)]
     lib.rt_render.argtypes = [C.c_void_p, C.POINTER(_capi.rt_camera_desc), C.POINTER(_capi.rt_render_params),

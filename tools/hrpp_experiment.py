@@ -29,7 +29,7 @@ def main():
     a = ap.parse_args()
     base = rt.CONFIGS[a.config]
     cfg = base.scaled(a.width or base.width, a.spp or base.spp)
-    os.environ["RT_HRPP_SLOT_BITS"] = str(a.bits)
+    rt.set_option("hrpp_slot_bits", a.bits)
     scene = rt.Scene.generate(cfg.scene, cfg.scene_seed)
     ds = rt.DeviceScene(scene)
     out = {"config": cfg.name, "width": cfg.width, "height": cfg.height, "spp": cfg.spp, "slot_bits": a.bits}

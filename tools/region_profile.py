@@ -39,6 +39,9 @@ def main():
         sys.exit("set RT_LIBRARY to the _prof or _audit build")
     import torch
     import raytracinginoneweekendinrust_amd as rt
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import rtopts
+    rtopts.apply(rt)
     cfg = rt.CONFIGS[args.config]
     if args.spp:
         cfg = cfg.scaled(cfg.width, args.spp)
@@ -62,7 +65,7 @@ def main():
         captured = tf.read().splitlines()
         lines = [ln for ln in captured if ln.startswith('{"rt_profile"')]
         for ln in captured:
-            if ln.startswith(('{"leaf_audit', '{"audit', '{"trav_audit', '{"trips_hist')):
+            if ln.startswith(('{"leaf_audit', '{"audit', '{"trav_audit', '{"bounds_audit', '{"trips_hist')):
                 print(ln)
     if not lines:  # an audit build: no region counters
         return

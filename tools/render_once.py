@@ -22,6 +22,9 @@ def main():
     ap.add_argument("--exact-bvh", action="store_true")
     a = ap.parse_args()
     import raytracinginoneweekendinrust_amd as rt
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import rtopts
+    rtopts.apply(rt)  # RT_TUNE=... etc. of the session scripts -> rt_set_option
     cfg = rt.CONFIGS[a.config]
     cfg = cfg.scaled(a.width or cfg.width, a.spp or cfg.spp)
     scene = rt.Scene.generate(cfg.scene, cfg.scene_seed)
