@@ -1652,9 +1652,10 @@ RT_DEV bool near_zero(V v) {  // utils.rs:5-7
     const float eps = 1.1920929e-07f;
     return __builtin_fabsf(v.x) < eps && __builtin_fabsf(v.y) < eps && __builtin_fabsf(v.z) < eps;
 }
+// att_later: the caller evaluates a Marble attenuation itself (after the wave-wide turbulence).
 template <bool kTurb = false>
 RT_DEV bool scatter(const DevScene& S, const DevMaterial& m, const Ray& r, const Rec& rec, Rng& g, const Key& k,
-                    V& att, Ray& sc, uint32_t tex = 0u, double turb = 0.0) {
+                    V& att, Ray& sc, uint32_t tex = 0u, double turb = 0.0, bool att_later = false) {
     sc.o = rec.p;
     sc.time = r.time;
     // Lambertian, Metal and Isotropic each draw exactly one in_unit_sphere() and
@@ -1670,7 +1671,7 @@ RT_DEV bool scatter(const DevScene& S, const DevMaterial& m, const Ray& r, const
         V dir = rec.n + normalize(rs);
         if (near_zero(dir)) dir = rec.n;
         sc.d = dir;
-        att = tex_value<kTurb>(S, kTurb ? tex : m.tex, rec.u, rec.v, rec.p, turb);
+        if (!att_later) att = tex_value<kTurb>(S, kTurb ? tex : m.tex, rec.u, rec.v, rec.p, turb);
         PROF_ADD(kPrLambert, pb);
         return true;
     }
@@ -1707,7 +1708,7 @@ RT_DEV bool scatter(const DevScene& S, const DevMaterial& m, const Ray& r, const
     if (m.kind == rtdev::kMatIsotropic) {  // isotropic.rs:31-43
         PROF_T0(ps);
         sc.d = rs;
-        att = tex_value<kTurb>(S, kTurb ? tex : m.tex, rec.u, rec.v, rec.p, turb);
+        if (!att_later) att = tex_value<kTurb>(S, kTurb ? tex : m.tex, rec.u, rec.v, rec.p, turb);
         PROF_ADD(kPrIso, ps);
         return true;
     }
@@ -1955,49 +1956,8 @@ RT_DEV bool take_sample(ItemPool& pool, bool want, const DevCamera& C, const Dev
 
 // The end of a segment whose list walk is complete (ray.rs:43-61): background,
 // or HitRecord + emit + scatter. Returns true when the path ends; its radiance is
-// then stored in the sample buffer.
-// The same end of a segment with the HitRecord already built (rec, when any) and the
-// material's texture already resolved through its Checkers (tex) for the instances
-// that evaluate Marble turbulence wave-wide: the caller passed `turb` from
-// turbulence_wave for a Marble hit (kFMarble).
-RT_DEV bool finish_segment_rec(const DevScene& S, const DevParams& P, const ChunkParams& Q, const Key& k,
-                               float* __restrict__ sbuf, bool any, const Rec& rec, uint32_t tex, double turb, Ray& ray,
-                               V& L, V& T, uint32_t& depth, Rng& g, uint32_t pixel, uint32_t s_local) {
-    PROF_T0(pg);
-    bool done;
-    if (!any) {
-        L = L + T * mk(P.bg[0], P.bg[1], P.bg[2]);
-        done = true;
-    } else {
-        const DevMaterial m = S.mats[rec.mat];
-        PROF_T0(pm);
-        V em = m.kind == rtdev::kMatLight ? tex_value<true>(S, tex, rec.u, rec.v, rec.p, turb) : mk(0.0f, 0.0f, 0.0f);
-        L = L + T * em;
-        PROF_ADD(kPrEmit, pm);
-        V att;
-        Ray sc;
-        PROF_T0(ps);
-        bool scattered = scatter<true>(S, m, ray, rec, g, k, att, sc, tex, turb);
-        PROF_ADD(kPrScatter, ps);
-        if (scattered) {
-            T = T * att;
-            ray = sc;
-            depth -= 1u;
-            done = depth == 0u;
-        } else {
-            done = true;
-        }
-    }
-    if (done) {
-        float* o = sbuf + ((size_t)s_local * Q.npix + pixel) * 3u;
-        o[0] = L.x;
-        o[1] = L.y;
-        o[2] = L.z;
-    }
-    PROF_ADD(kPrSegment, pg);
-    return done;
-}
-
+// then stored in the sample buffer. (Instances with kFMarble do this inline in
+// trace_samples, around the wave-wide turbulence.)
 template <uint32_t kF = kFAll>
 RT_DEV bool finish_segment(const DevScene& S, const DevParams& P, const ChunkParams& Q, const Key& k,
                            float* __restrict__ sbuf, bool any, uint32_t he, uint32_t hc, float t, Ray& ray, V& L, V& T,
@@ -2039,6 +1999,73 @@ RT_DEV bool finish_segment(const DevScene& S, const DevParams& P, const ChunkPar
     }
     PROF_ADD(kPrSegment, pg);
     return done;
+}
+
+// The end of a segment (ray.rs:43-61) for instances with kFMarble: HitRecord, emission and
+// scatter per lane, where a lane whose texture resolves to a Marble leaves only its
+// attenuation (or, for a light, its emission) for after turbulence_wave, so the HitRecord
+// is dead while the wave evaluates the turbulence together. The draws and every value are
+// finish_segment's (the Marble value is tex_value's 0.5 * (1 + sin(scale * p.z + 10 * turb))).
+// All 64 lanes must call it (turbulence_wave is convergent); lanes without `shade` only
+// join the turbulence. Returns true when the lane's path ended (its sample is stored).
+template <uint32_t kF>
+RT_DEV bool shade_marble(const DevScene& S, const DevParams& P, const ChunkParams& Q, const Key& k,
+                         float* __restrict__ sbuf, bool shade, bool any, uint32_t he, uint32_t hc, float t, Ray& ray,
+                         V& L, V& T, uint32_t& depth, Rng& g, uint32_t pixel, uint32_t s_local) {
+    bool marble = false, mlight = false, scattered = false, done = false;
+    V mp = mk(0.0f, 0.0f, 0.0f);
+    uint32_t tab = 0u;
+    float mscale = 0.0f;
+    if (shade && !any) {  // ray.rs:45-47
+        L = L + T * mk(P.bg[0], P.bg[1], P.bg[2]);
+        done = true;
+    } else if (shade) {
+        Rec rec;
+        PROF_T0(pc);
+        make_record<kF>(S, he, hc, t, ray, rec);
+        PROF_ADD(kPrRecord, pc);
+        const DevMaterial m = S.mats[rec.mat];
+        uint32_t tex = m.tex;
+        if (m.kind == rtdev::kMatLight || m.kind == rtdev::kMatLambertian || m.kind == rtdev::kMatIsotropic) {
+            tex = tex_resolve(S, m.tex, rec.p);
+            const DevTexture& tx = S.texs[tex];
+            marble = tx.kind == rtdev::kTexMarble;
+            tab = tx.a;
+            mscale = tx.scale;
+        }
+        mp = rec.p;
+        mlight = m.kind == rtdev::kMatLight;
+        if (!(marble && mlight)) {  // ray.rs:50 emitted (a Marble light's after the turbulence)
+            const V em = mlight ? tex_value<true>(S, tex, rec.u, rec.v, rec.p, 0.0) : mk(0.0f, 0.0f, 0.0f);
+            L = L + T * em;
+        }
+        V att;
+        Ray sc;
+        scattered = scatter<true>(S, m, ray, rec, g, k, att, sc, tex, 0.0, marble);
+        if (scattered) {
+            if (!marble) T = T * att;
+            ray = sc;
+            depth -= 1u;
+            done = depth == 0u;
+        } else {
+            done = true;
+        }
+    }
+    PROF_T0(pmw);
+    const double turb = turbulence_wave(S.perm, marble, mp, tab);
+    PROF_ADD(kPrMarble, pmw);
+    if (marble) {  // marble.rs:23-29
+        const float sv = 0.5f * (1.0f + rt_sinf(mscale * mp.z + 10.0f * (float)turb));
+        if (mlight) L = L + T * mk(sv, sv, sv);
+        else if (scattered) T = T * mk(sv, sv, sv);
+    }
+    if (shade && done) {
+        float* o = sbuf + ((size_t)s_local * Q.npix + pixel) * 3u;
+        o[0] = L.x;
+        o[1] = L.y;
+        o[2] = L.z;
+    }
+    return shade && done;
 }
 
 // Every live lane traces one whole segment per loop trip: the list walk with its
@@ -2145,23 +2172,8 @@ __global__ __launch_bounds__(64, kWaves) void trace_samples(DevScene Sg, DevCame
             }
             const bool walked = has && w.pos == S.num_top;
             if constexpr ((kF & kFMarble) != 0u) {
-                Rec rec;
-                rec.p = mk(0.0f, 0.0f, 0.0f);
-                uint32_t tex = 0u, tab = 0u;
-                bool marble = false;
-                if (walked && w.any) {
-                    make_record<kF>(S, w.hit_entry, w.hit_code, w.closest, ray, rec);
-                    const DevMaterial& m = S.mats[rec.mat];
-                    if (m.kind == rtdev::kMatLight || m.kind == rtdev::kMatLambertian || m.kind == rtdev::kMatIsotropic) {
-                        tex = tex_resolve(S, m.tex, rec.p);
-                        const DevTexture& tx = S.texs[tex];
-                        marble = tx.kind == rtdev::kTexMarble;
-                        tab = tx.a;
-                    }
-                }
-                const double turb = turbulence_wave(S.perm, marble, rec.p, tab);
-                if (walked &&
-                    finish_segment_rec(S, P, Q, k, sbuf, w.any, rec, tex, turb, ray, L, T, depth, g, pixel, s_local)) {
+                if (shade_marble<kF>(S, P, Q, k, sbuf, walked, w.any, w.hit_entry, w.hit_code, w.closest, ray, L, T,
+                                     depth, g, pixel, s_local)) {
                     has = false;
                     nseg += nseg_sample;
                 }
@@ -2183,17 +2195,11 @@ __global__ __launch_bounds__(64, kWaves) void trace_samples(DevScene Sg, DevCame
         PROF_ADD(kPrRefill, pr);
         if (__ballot(has) == 0ull) break;  // pool exhausted and every path finished
         if constexpr ((kF & kFMarble) != 0u) {
-            // world walk and HitRecord per lane, then the Marble turbulence of every lane that
-            // needs it evaluated by the whole (converged) wave, then emit / scatter per lane
             bool shade = false, any = false;
-            Rec rec;
-            rec.p = mk(0.0f, 0.0f, 0.0f);
-            uint32_t tex = 0u, tab = 0u;
-            bool marble = false;
+            float t = 0.0f;
+            uint32_t he = 0, hc = 0;
             if (has) {
                 nseg_sample += 1u;
-                float t;
-                uint32_t he = 0, hc = 0;
                 bool replay = false;
                 PROF_T0(pw);
                 any = world_hit<kKind, kF>(S, P.prune_delta, ray, g, k, t, he, hc, stk, mode, replay);
@@ -2204,29 +2210,9 @@ __global__ __launch_bounds__(64, kWaves) void trace_samples(DevScene Sg, DevCame
                     has = false;
                 } else {
                     shade = true;
-                    if (any) {
-                        PROF_T0(pc);
-                        make_record<kF>(S, he, hc, t, ray, rec);
-                        PROF_ADD(kPrRecord, pc);
-                        const DevMaterial& m = S.mats[rec.mat];
-                        if (m.kind == rtdev::kMatLight || m.kind == rtdev::kMatLambertian ||
-                            m.kind == rtdev::kMatIsotropic) {
-                            tex = tex_resolve(S, m.tex, rec.p);
-                            const DevTexture& tx = S.texs[tex];
-                            marble = tx.kind == rtdev::kTexMarble;
-                            tab = tx.a;
-                        }
-                    }
                 }
             }
-            PROF_T0(pmw);
-            double turb = 0.0;
-#ifdef RT_TURB_NOINLINE
-            if (__ballot(marble))
-#endif
-                turb = turbulence_wave(S.perm, marble, rec.p, tab);
-            PROF_ADD(kPrMarble, pmw);
-            if (shade && finish_segment_rec(S, P, Q, k, sbuf, any, rec, tex, turb, ray, L, T, depth, g, pixel, s_local)) {
+            if (shade_marble<kF>(S, P, Q, k, sbuf, shade, any, he, hc, t, ray, L, T, depth, g, pixel, s_local)) {
                 has = false;
                 nseg += nseg_sample;
             }
