@@ -2135,8 +2135,10 @@ __global__ __launch_bounds__(64, kWaves) void trace_samples(DevScene Sg, DevCame
         }
     }
     bool has = false;
-    uint32_t pixel = 0, s_local = 0, depth = 0;
-    unsigned long long nseg = 0, nseg_sample = 0;
+    // A lane's pixel and chunk-local sample are its Rng's counter fields (start_sample sets
+    // them), so they are not kept a second time; per-lane segment counts fit 32 bits.
+    uint32_t take_pixel = 0, take_sample_idx = 0, depth = 0;
+    uint32_t nseg = 0, nseg_sample = 0;
     V L = mk(0.0f, 0.0f, 0.0f), T = mk(1.0f, 1.0f, 1.0f);
     Rng g{};
     Ray ray{};
@@ -2147,7 +2149,7 @@ __global__ __launch_bounds__(64, kWaves) void trace_samples(DevScene Sg, DevCame
         w.pos = 0u;
         for (;;) {
             PROF_T0(pr);
-            if (take_sample(pool, !has, C, P, Q, k, counter, list, list_n, sbuf, lane, pixel, s_local, L, T, depth, g,
+            if (take_sample(pool, !has, C, P, Q, k, counter, list, list_n, sbuf, lane, take_pixel, take_sample_idx, L, T, depth, g,
                             ray)) {
                 has = true;
                 nseg_sample = 0;
@@ -2167,18 +2169,18 @@ __global__ __launch_bounds__(64, kWaves) void trace_samples(DevScene Sg, DevCame
             PROF_ADD(kPrWorld, pw);
             if (has && replay) {  // hand the sample to the reference kernel
                 unsigned idx = atomicAdd(&ctr->replay_count, 1u);
-                if (idx < kReplayCap) replay_list[idx] = ReplayItem{pixel, s_local};
+                if (idx < kReplayCap) replay_list[idx] = ReplayItem{g.pixel, g.sample - Q.sample0};
                 has = false;
             }
             const bool walked = has && w.pos == S.num_top;
             if constexpr ((kF & kFMarble) != 0u) {
                 if (shade_marble<kF>(S, P, Q, k, sbuf, walked, w.any, w.hit_entry, w.hit_code, w.closest, ray, L, T,
-                                     depth, g, pixel, s_local)) {
+                                     depth, g, g.pixel, g.sample - Q.sample0)) {
                     has = false;
                     nseg += nseg_sample;
                 }
             } else if (walked && finish_segment<kF>(S, P, Q, k, sbuf, w.any, w.hit_entry, w.hit_code, w.closest, ray, L,
-                                                    T, depth, g, pixel, s_local)) {
+                                                    T, depth, g, g.pixel, g.sample - Q.sample0)) {
                 has = false;
                 nseg += nseg_sample;
             }
@@ -2187,7 +2189,7 @@ __global__ __launch_bounds__(64, kWaves) void trace_samples(DevScene Sg, DevCame
     } else
     for (;;) {
         PROF_T0(pr);
-        if (take_sample(pool, !has, C, P, Q, k, counter, list, list_n, sbuf, lane, pixel, s_local, L, T, depth, g,
+        if (take_sample(pool, !has, C, P, Q, k, counter, list, list_n, sbuf, lane, take_pixel, take_sample_idx, L, T, depth, g,
                         ray)) {
             has = true;
             nseg_sample = 0;
@@ -2206,13 +2208,13 @@ __global__ __launch_bounds__(64, kWaves) void trace_samples(DevScene Sg, DevCame
                 PROF_ADD(kPrWorld, pw);
                 if (kKind == 0 && replay) {  // hand the sample to the reference kernel
                     unsigned idx = atomicAdd(&ctr->replay_count, 1u);
-                    if (idx < kReplayCap) replay_list[idx] = ReplayItem{pixel, s_local};
+                    if (idx < kReplayCap) replay_list[idx] = ReplayItem{g.pixel, g.sample - Q.sample0};
                     has = false;
                 } else {
                     shade = true;
                 }
             }
-            if (shade_marble<kF>(S, P, Q, k, sbuf, shade, any, he, hc, t, ray, L, T, depth, g, pixel, s_local)) {
+            if (shade_marble<kF>(S, P, Q, k, sbuf, shade, any, he, hc, t, ray, L, T, depth, g, g.pixel, g.sample - Q.sample0)) {
                 has = false;
                 nseg += nseg_sample;
             }
@@ -2226,9 +2228,9 @@ __global__ __launch_bounds__(64, kWaves) void trace_samples(DevScene Sg, DevCame
             PROF_ADD(kPrWorld, pw);
             if (kKind == 0 && replay) {  // hand the sample to the reference kernel
                 unsigned idx = atomicAdd(&ctr->replay_count, 1u);
-                if (idx < kReplayCap) replay_list[idx] = ReplayItem{pixel, s_local};
+                if (idx < kReplayCap) replay_list[idx] = ReplayItem{g.pixel, g.sample - Q.sample0};
                 has = false;
-            } else if (finish_segment<kF>(S, P, Q, k, sbuf, any, he, hc, t, ray, L, T, depth, g, pixel, s_local)) {
+            } else if (finish_segment<kF>(S, P, Q, k, sbuf, any, he, hc, t, ray, L, T, depth, g, g.pixel, g.sample - Q.sample0)) {
                 has = false;
                 nseg += nseg_sample;
             }
@@ -2239,7 +2241,7 @@ __global__ __launch_bounds__(64, kWaves) void trace_samples(DevScene Sg, DevCame
         if (lane < 4u * S.hrpp_npred) atomicAdd(&S.hrpp_stats[lane], (unsigned long long)S.hrpp_cnt[lane]);
     }
     if (seg_counter) {
-        unsigned long long v = nseg;
+        unsigned long long v = (unsigned long long)nseg;
         for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
         if (lane == 0u) {
             atomicAdd(seg_counter, v);
