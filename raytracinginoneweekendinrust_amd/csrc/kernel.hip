@@ -1742,20 +1742,28 @@ RT_DEV void start_sample(const DevCamera& C, const DevParams& P, const Key& k, u
 }
 
 // One launch covers samples [sample0, sample0 + samples) of every pixel of the shard.
-// Work items are (8x8 block, sample, pixel-in-block); a "batch" is `group`
-// consecutive samples of one block (64 * group items), blocks in shard order.
-// Longer batches keep a wave on one block longer (more coherent paths) but waste
-// the slots of a partial last batch: 16 samples from 256 spp up, else 8 (measured on
-// C3: 16 is 1.3% faster than 8 at 500 spp, 8 is 5% faster than 16 at 100 spp).
-static inline uint32_t batch_group(uint32_t samples) { return samples >= 256u ? 16u : 8u; }
+// Work units are (8x8 block, sample) pairs, block-major; a batch is up to `group` consecutive
+// units (64 items each) that a wave takes with one atomic and feeds to its idle lanes.
+// The best batch size follows the work per wave: the power of two at or below 1/64 of the
+// units each resident wave will process, within [4, 16]. Measured on C3 (same box, units per
+// wave -> ms per launch for batch sizes): 1831 (500 spp, one GPU) -> 16: 511, 8: 518, 32: 540;
+// 915 (250 spp, or one rank of two) -> 8: 264, 12: 270, 16: 278; 458 (rank of four) -> 4: 138,
+// 8: 144; 366 (100 spp) -> 4: 112, 8: 119; 230 (63 spp, or one rank of eight) -> 2: 77, 4: 74,
+// 8: 82, 16: 97. The fixed 16 cost an 8-GPU rank a third of its time.
+static inline uint32_t batch_group(uint64_t units, uint32_t waves) {
+    const uint64_t per = units / ((uint64_t)(waves ? waves : 1u) * 64u);
+    uint32_t g = 4u;
+    while (g < 16u && 2u * g <= per) g *= 2u;
+    return g;
+}
 constexpr uint32_t kPermLdsMax = 4u * 9u * 256u;  // up to four Marble textures staged in LDS
 struct ChunkParams {
     uint32_t sample0;         // global sample index of chunk sample 0 (includes P.sample_base)
     uint32_t samples;         // samples per pixel in this chunk
-    uint32_t groups_per_block;
-    uint32_t num_batches;
-    uint32_t npix;            // width * height (sample-buffer plane size)
-    uint32_t group;           // samples per batch (batch_group)
+    uint32_t units;           // work units: (8x8 block of the shard, sample) pairs, block-major
+    uint32_t pad;
+    uint32_t nslots;          // sample-buffer plane size: 64 slots per 8x8 block of the shard, block-major
+    uint32_t group;           // units per batch at most (batch_group)
 };
 
 // HittableList::hit over the world (hittable.rs:100-118), t in [0.001, inf).
@@ -1872,7 +1880,7 @@ RT_DEV void world_walk(const DevScene& S, float delta, const Ray& ray, Rng& g, c
 // resolve_samples() then sums every pixel's samples IN SAMPLE ORDER, exactly like
 // `color_accumulator +=` in the reference.
 struct ItemPool {  // wave-uniform
-    uint32_t batch, next, end;
+    uint32_t batch, next, end;  // batch = its first unit; next / end: items (64 per unit) of the batch
     bool exhausted;
 };
 // Per-chunk device counters of the trace stage (zeroed before each chunk).
@@ -1894,54 +1902,80 @@ struct ReplayItem {
 // 64 at a time through *counter).
 RT_DEV bool take_sample(ItemPool& pool, bool want, const DevCamera& C, const DevParams& P, const ChunkParams& Q,
                         const Key& k, unsigned* counter, const ReplayItem* list, uint32_t list_n, float* sbuf,
-                        uint32_t lane, uint32_t& pixel, uint32_t& s_local, V& L, V& T, uint32_t& depth, Rng& g,
+                        uint32_t lane, uint32_t& slot, uint32_t& s_local, V& L, V& T, uint32_t& depth, Rng& g,
                         Ray& ray) {
     bool got = false;
     for (;;) {
         unsigned long long need = __ballot(want && !got);
         if (need == 0ull || pool.exhausted) break;
         if (pool.next == pool.end) {
-            uint32_t bt = 0;
-            if (lane == 0u) bt = atomicAdd(counter, list ? 64u : 1u);
+            // Guided batches: up to Q.group units while work is plentiful, shrinking with the
+            // work left (rem / (2 x waves), at least one unit) so that the waves finish together
+            // instead of the last ones draining a full batch alone.
+            uint32_t bt = 0, cnt = 64u;
+            if (lane == 0u) {
+                if (list) {
+                    bt = atomicAdd(counter, 64u);
+                } else {
+                    const uint32_t cur = __hip_atomic_load(counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const uint32_t rem = cur < Q.units ? Q.units - cur : 0u;
+                    cnt = rem / (2u * gridDim.x);
+                    cnt = cnt < 1u ? 1u : (cnt > Q.group ? Q.group : cnt);
+                    bt = atomicAdd(counter, cnt);
+                }
+            }
             bt = __builtin_amdgcn_readfirstlane(bt);
-            if (bt >= (list ? list_n : Q.num_batches)) {
+            cnt = __builtin_amdgcn_readfirstlane(cnt);
+            if (bt >= (list ? list_n : Q.units)) {
                 pool.exhausted = true;
                 break;
             }
             pool.batch = bt;
             pool.next = list ? bt : 0u;
-            pool.end = list ? (bt + 64u < list_n ? bt + 64u : list_n) : 64u * Q.group;
+            pool.end = list ? (bt + 64u < list_n ? bt + 64u : list_n) : 64u * cnt;
             continue;
         }
         uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
         uint32_t avail = pool.end - pool.next;
         if (want && !got && rank < avail) {
-            uint32_t x, y, s;
+            uint32_t x, y, s, sl;
             if (list) {
                 const ReplayItem it = list[pool.next + rank];
                 y = it.pixel / P.width;
                 x = it.pixel - y * P.width;
                 s = it.sample;
+                const uint32_t blk = (y >> 3) * P.blocks_x + (x >> 3);
+                sl = ((blk - P.shard_index) / P.shard_count) * 64u + ((y & 7u) << 3) + (x & 7u);
             } else {
-                uint32_t item = pool.next + rank;
-                uint32_t blk_local = pool.batch / Q.groups_per_block;
-                uint32_t grp = pool.batch - blk_local * Q.groups_per_block;
-                s = grp * Q.group + (item >> 6);
+                // unit pool.batch + (item >> 6); a batch (<= Q.group <= Q.samples units) crosses at
+                // most one block boundary, so the batch's block and sample are divided once
+                const uint32_t item = pool.next + rank;
+                const uint32_t blk0 = __builtin_amdgcn_readfirstlane(pool.batch / Q.samples);
+                const uint32_t s0 = pool.batch - blk0 * Q.samples;
+                s = s0 + (item >> 6);
+                uint32_t blk_local = blk0;
+                if (s >= Q.samples) {
+                    s -= Q.samples;
+                    blk_local += 1u;
+                }
+                if (pool.batch + (item >> 6) >= Q.units) s = Q.samples;  // past the last unit: no work
                 uint32_t pib = item & 63u;
+                sl = blk_local * 64u + pib;
                 uint32_t blk = P.shard_index + blk_local * P.shard_count;
                 uint32_t by = blk / P.blocks_x, bx = blk - by * P.blocks_x;
                 x = bx * 8u + (pib & 7u);
                 y = by * 8u + (pib >> 3);
             }
             if (x < P.width && y < P.height && s < Q.samples) {
-                pixel = y * P.width + x;
+                const uint32_t pixel = y * P.width + x;
+                slot = sl;
                 s_local = s;
                 L = mk(0.0f, 0.0f, 0.0f);
                 T = mk(1.0f, 1.0f, 1.0f);
                 depth = P.max_depth;
                 start_sample(C, P, k, x, y, pixel, Q.sample0 + s, g, ray);
                 if (depth == 0u) {
-                    float* o = sbuf + ((size_t)s_local * Q.npix + pixel) * 3u;
+                    float* o = sbuf + ((size_t)s_local * Q.nslots + sl) * 3u;
                     o[0] = o[1] = o[2] = 0.0f;
                 } else {
                     got = true;
@@ -1961,7 +1995,7 @@ RT_DEV bool take_sample(ItemPool& pool, bool want, const DevCamera& C, const Dev
 template <uint32_t kF = kFAll>
 RT_DEV bool finish_segment(const DevScene& S, const DevParams& P, const ChunkParams& Q, const Key& k,
                            float* __restrict__ sbuf, bool any, uint32_t he, uint32_t hc, float t, Ray& ray, V& L, V& T,
-                           uint32_t& depth, Rng& g, uint32_t pixel, uint32_t s_local) {
+                           uint32_t& depth, Rng& g, uint32_t slot, uint32_t s_local) {
     PROF_T0(pg);
     bool done;
     if (!any) {
@@ -1992,7 +2026,7 @@ RT_DEV bool finish_segment(const DevScene& S, const DevParams& P, const ChunkPar
         }
     }
     if (done) {
-        float* o = sbuf + ((size_t)s_local * Q.npix + pixel) * 3u;
+        float* o = sbuf + ((size_t)s_local * Q.nslots + slot) * 3u;
         o[0] = L.x;
         o[1] = L.y;
         o[2] = L.z;
@@ -2011,7 +2045,7 @@ RT_DEV bool finish_segment(const DevScene& S, const DevParams& P, const ChunkPar
 template <uint32_t kF>
 RT_DEV bool shade_marble(const DevScene& S, const DevParams& P, const ChunkParams& Q, const Key& k,
                          float* __restrict__ sbuf, bool shade, bool any, uint32_t he, uint32_t hc, float t, Ray& ray,
-                         V& L, V& T, uint32_t& depth, Rng& g, uint32_t pixel, uint32_t s_local) {
+                         V& L, V& T, uint32_t& depth, Rng& g, uint32_t slot, uint32_t s_local) {
     bool marble = false, mlight = false, scattered = false, done = false;
     V mp = mk(0.0f, 0.0f, 0.0f);
     uint32_t tab = 0u;
@@ -2060,7 +2094,7 @@ RT_DEV bool shade_marble(const DevScene& S, const DevParams& P, const ChunkParam
         else if (scattered) T = T * mk(sv, sv, sv);
     }
     if (shade && done) {
-        float* o = sbuf + ((size_t)s_local * Q.npix + pixel) * 3u;
+        float* o = sbuf + ((size_t)s_local * Q.nslots + slot) * 3u;
         o[0] = L.x;
         o[1] = L.y;
         o[2] = L.z;
@@ -2137,7 +2171,7 @@ __global__ __launch_bounds__(64, kWaves) void trace_samples(DevScene Sg, DevCame
     bool has = false;
     // A lane's pixel and chunk-local sample are its Rng's counter fields (start_sample sets
     // them), so they are not kept a second time; per-lane segment counts fit 32 bits.
-    uint32_t take_pixel = 0, take_sample_idx = 0, depth = 0;
+    uint32_t slot = 0, take_sample_idx = 0, depth = 0;  // slot: the sample-buffer slot of the lane's pixel
     uint32_t nseg = 0, nseg_sample = 0;
     V L = mk(0.0f, 0.0f, 0.0f), T = mk(1.0f, 1.0f, 1.0f);
     Rng g{};
@@ -2149,7 +2183,7 @@ __global__ __launch_bounds__(64, kWaves) void trace_samples(DevScene Sg, DevCame
         w.pos = 0u;
         for (;;) {
             PROF_T0(pr);
-            if (take_sample(pool, !has, C, P, Q, k, counter, list, list_n, sbuf, lane, take_pixel, take_sample_idx, L, T, depth, g,
+            if (take_sample(pool, !has, C, P, Q, k, counter, list, list_n, sbuf, lane, slot, take_sample_idx, L, T, depth, g,
                             ray)) {
                 has = true;
                 nseg_sample = 0;
@@ -2175,12 +2209,12 @@ __global__ __launch_bounds__(64, kWaves) void trace_samples(DevScene Sg, DevCame
             const bool walked = has && w.pos == S.num_top;
             if constexpr ((kF & kFMarble) != 0u) {
                 if (shade_marble<kF>(S, P, Q, k, sbuf, walked, w.any, w.hit_entry, w.hit_code, w.closest, ray, L, T,
-                                     depth, g, g.pixel, g.sample - Q.sample0)) {
+                                     depth, g, slot, g.sample - Q.sample0)) {
                     has = false;
                     nseg += nseg_sample;
                 }
             } else if (walked && finish_segment<kF>(S, P, Q, k, sbuf, w.any, w.hit_entry, w.hit_code, w.closest, ray, L,
-                                                    T, depth, g, g.pixel, g.sample - Q.sample0)) {
+                                                    T, depth, g, slot, g.sample - Q.sample0)) {
                 has = false;
                 nseg += nseg_sample;
             }
@@ -2189,7 +2223,7 @@ __global__ __launch_bounds__(64, kWaves) void trace_samples(DevScene Sg, DevCame
     } else
     for (;;) {
         PROF_T0(pr);
-        if (take_sample(pool, !has, C, P, Q, k, counter, list, list_n, sbuf, lane, take_pixel, take_sample_idx, L, T, depth, g,
+        if (take_sample(pool, !has, C, P, Q, k, counter, list, list_n, sbuf, lane, slot, take_sample_idx, L, T, depth, g,
                         ray)) {
             has = true;
             nseg_sample = 0;
@@ -2214,7 +2248,7 @@ __global__ __launch_bounds__(64, kWaves) void trace_samples(DevScene Sg, DevCame
                     shade = true;
                 }
             }
-            if (shade_marble<kF>(S, P, Q, k, sbuf, shade, any, he, hc, t, ray, L, T, depth, g, g.pixel, g.sample - Q.sample0)) {
+            if (shade_marble<kF>(S, P, Q, k, sbuf, shade, any, he, hc, t, ray, L, T, depth, g, slot, g.sample - Q.sample0)) {
                 has = false;
                 nseg += nseg_sample;
             }
@@ -2230,7 +2264,7 @@ __global__ __launch_bounds__(64, kWaves) void trace_samples(DevScene Sg, DevCame
                 unsigned idx = atomicAdd(&ctr->replay_count, 1u);
                 if (idx < kReplayCap) replay_list[idx] = ReplayItem{g.pixel, g.sample - Q.sample0};
                 has = false;
-            } else if (finish_segment<kF>(S, P, Q, k, sbuf, any, he, hc, t, ray, L, T, depth, g, g.pixel, g.sample - Q.sample0)) {
+            } else if (finish_segment<kF>(S, P, Q, k, sbuf, any, he, hc, t, ray, L, T, depth, g, slot, g.sample - Q.sample0)) {
                 has = false;
                 nseg += nseg_sample;
             }
@@ -2255,15 +2289,18 @@ __global__ __launch_bounds__(64, kWaves) void trace_samples(DevScene Sg, DevCame
 // Chunks continue the same running sum held in `out`.
 __global__ __launch_bounds__(256) void resolve_samples(const float* __restrict__ sbuf, float* __restrict__ out,
                                                         DevParams P, ChunkParams Q, int first, int last) {
-    uint32_t p = blockIdx.x * 256u + threadIdx.x;
-    if (p >= Q.npix) return;
-    uint32_t y = p / P.width, x = p - y * P.width;
-    uint32_t blk = (y >> 3) * P.blocks_x + (x >> 3);
-    if (P.shard_count > 1u && blk % P.shard_count != P.shard_index) return;
-    float* o = out + (size_t)p * 3u;
+    // one thread per sample-buffer slot (block-major: 64 consecutive slots are one 8x8 block,
+    // so every plane is read in full, coalesced lines)
+    const uint32_t t = blockIdx.x * 256u + threadIdx.x;
+    if (t >= Q.nslots) return;
+    const uint32_t blk = P.shard_index + (t >> 6) * P.shard_count, pib = t & 63u;
+    const uint32_t by = blk / P.blocks_x, bx = blk - by * P.blocks_x;
+    const uint32_t x = bx * 8u + (pib & 7u), y = by * 8u + (pib >> 3);
+    if (x >= P.width || y >= P.height) return;
+    float* o = out + ((size_t)y * P.width + x) * 3u;
     V acc = first ? mk(0.0f, 0.0f, 0.0f) : mk(o[0], o[1], o[2]);
-    const float* src = sbuf + (size_t)p * 3u;
-    const size_t plane = (size_t)Q.npix * 3u;
+    const float* src = sbuf + (size_t)t * 3u;
+    const size_t plane = (size_t)Q.nslots * 3u;
     for (uint32_t s = 0; s < Q.samples; ++s) {
         acc = acc + mk(src[0], src[1], src[2]);
         src += plane;
@@ -2837,8 +2874,9 @@ int rt_render_launch_camera(rt_scene_handle s, const rt_camera* camera, const rt
     }
     if ((e = hipStreamWaitEvent((hipStream_t)stream, s->done, 0)) != hipSuccess) return hip_fail(e, "hipStreamWaitEvent");
     // Sample buffer: chunks of whole sample ranges (the per-pixel sum stays in order).
-    const uint64_t npix = (uint64_t)p->width * p->height;
-    const uint64_t per_sample = npix * 3u * sizeof(float);
+    // the shard's 8x8 blocks, 64 slots each, block-major (dense for every shard: full cache lines)
+    const uint64_t nslots = (uint64_t)nblk * 64u;
+    const uint64_t per_sample = nslots * 3u * sizeof(float);
     // One launch per frame whenever HBM allows (each chunk ends with its own drain tail):
     // up to 40% of the free HBM, at least 8 GiB (C4's 1000-spp frame needs 24.9 GB, C5's 49.8 GB)
     uint64_t budget = 8192ull << 20;
@@ -2853,6 +2891,7 @@ int rt_render_launch_camera(rt_scene_handle s, const rt_camera* camera, const rt
     }
     if (const int64_t mb = opt(RT_OPT_SAMPLE_BUFFER_MB)) budget = (uint64_t)mb << 20;
     uint64_t max_s = budget / per_sample;
+    if (max_s > 0x7fffffffull / nblk) max_s = 0x7fffffffull / nblk;  // (block, sample) units fit 31 bits
     if (max_s < 1) max_s = 1;
     uint32_t nchunks = (uint32_t)((p->samples_per_pixel + max_s - 1) / max_s);
     uint32_t chunk = (p->samples_per_pixel + nchunks - 1) / nchunks;
@@ -2947,16 +2986,17 @@ int rt_render_launch_camera(rt_scene_handle s, const rt_camera* camera, const rt
         ChunkParams q;
         q.sample0 = p->sample_base + c * chunk;
         q.samples = c + 1 < nchunks ? chunk : p->samples_per_pixel - c * chunk;
-        q.group = batch_group(q.samples);
+        q.units = (uint32_t)(nblk * (uint64_t)q.samples);
+        q.group = batch_group(q.units, exact || dev_ref.hrpp_tab ? (uint32_t)s->grid_ref : (uint32_t)s->grid);
         if (const int64_t gr = opt(RT_OPT_GROUP)) q.group = (uint32_t)gr;  // diagnostics / A-B runs
-        q.groups_per_block = (q.samples + q.group - 1) / q.group;
-        q.num_batches = nblk * q.groups_per_block;
-        q.npix = (uint32_t)npix;
+        if (q.group > q.samples) q.group = q.samples;  // a batch crosses at most one block boundary
+        q.pad = 0u;
+        q.nslots = (uint32_t)nslots;
         if ((e = hipMemsetAsync(s->counter, 0, sizeof(TraceCounters), st)) != hipSuccess)
             return hip_fail(e, "memset counters");
         uint32_t grid = (uint32_t)s->grid, grid_ref = (uint32_t)s->grid_ref;
-        if (grid > q.num_batches) grid = q.num_batches;
-        if (grid_ref > q.num_batches) grid_ref = q.num_batches;
+        if (grid > q.units) grid = q.units;
+        if (grid_ref > q.units) grid_ref = q.units;
         hipEvent_t* evp = nullptr;
         if (s->ev_count < rt_scene::kEvents) {
             evp = s->ev[s->ev_count];
@@ -3000,7 +3040,7 @@ int rt_render_launch_camera(rt_scene_handle s, const rt_camera* camera, const rt
             (void)hipEventRecord(evp[1], st);
             s->ev_count++;
         }
-        hipLaunchKernelGGL(resolve_samples, dim3((uint32_t)((npix + 255u) / 256u)), dim3(256), 0, st, s->sbuf, d_out, dp,
+        hipLaunchKernelGGL(resolve_samples, dim3((uint32_t)((nslots + 255u) / 256u)), dim3(256), 0, st, s->sbuf, d_out, dp,
                            q, c == 0 && !(p->flags & RT_FLAG_ACCUMULATE) ? 1 : 0,
                            c + 1 == nchunks && !(p->flags & RT_FLAG_RAW_SUM) ? 1 : 0);
         if ((e = hipGetLastError()) != hipSuccess) return hip_fail(e, "resolve_samples launch");
