@@ -143,6 +143,11 @@ def main() -> int:
     if not torch.cuda.is_available():
         log("bench.py needs a GPU (the HIP path has no CPU fallback)")
         return 2
+    # one GPU per rank; with fewer GPUs than ranks (a rehearsal on a one-GPU box) ranks share them
+    ndev = torch.cuda.device_count()
+    if local_rank >= ndev:
+        log(f"note: LOCAL_RANK {local_rank} >= {ndev} GPUs; rank shares GPU {local_rank % ndev}")
+    local_rank = local_rank % ndev
     torch.cuda.set_device(local_rank)
     if world > 1:  # gloo on the host: barriers and the max over ranks only; no collective on the data path
         dist.init_process_group("gloo", rank=rank, world_size=world)
