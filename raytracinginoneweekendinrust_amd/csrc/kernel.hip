@@ -25,6 +25,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <atomic>
 #include <mutex>
 #include <string>
@@ -84,6 +85,10 @@ constexpr uint32_t kAbLeaf2 = 1u << 8, kAbKeys2 = 1u << 9, kAbBvh2 = 1u << 10, k
 constexpr uint32_t kProfCopies = 64;  // flush targets spread over blockIdx to keep atomics uncontended
 constexpr uint32_t kProfWords = 3 * kPrCount + 16;  // region triples, then the two visit histograms
 __device__ unsigned long long g_prof[kProfCopies * kProfWords];
+// per-wave start / end clock (s_memrealtime, 100 MHz) of the fast kernel's last launch: the
+// ramp at the start and the drain at the end of a launch (tools/region_profile.py --waves)
+constexpr uint32_t kProfWaves = 8192;
+__device__ unsigned long long g_wave_t[2 * kProfWaves];
 __shared__ unsigned long long prof_lds[kProfWords];
 // per-traversal node-visit histograms (prof_lds[3 * kPrCount + bin]: lanes,
 // [3 * kPrCount + 8 + bin]: the wave's max per call); bins 0,1,2,3-4,5-8,9-16,17-32,33+
@@ -1899,7 +1904,8 @@ struct ReplayItem {
 // sample returns true with its camera ray started (renderer.rs:141-143); a
 // max_depth 0 sample (ray.rs:39-41: black, no segment) is stored and skipped.
 // With `list` set, the items are that many replay-list entries instead (pulled
-// 64 at a time through *counter).
+// through *counter in shares of ceil(list_n / waves), at most 64: the replayed
+// paths are few and long, and a wave's segment takes as long as its slowest lane).
 RT_DEV bool take_sample(ItemPool& pool, bool want, const DevCamera& C, const DevParams& P, const ChunkParams& Q,
                         const Key& k, unsigned* counter, const ReplayItem* list, uint32_t list_n, float* sbuf,
                         uint32_t lane, uint32_t& slot, uint32_t& s_local, V& L, V& T, uint32_t& depth, Rng& g,
@@ -1914,8 +1920,10 @@ RT_DEV bool take_sample(ItemPool& pool, bool want, const DevCamera& C, const Dev
             // instead of the last ones draining a full batch alone.
             uint32_t bt = 0, cnt = 64u;
             if (lane == 0u) {
-                if (list) {
-                    bt = atomicAdd(counter, 64u);
+                if (list) {  // a share of the list per wave: a replayed path runs with few others
+                    cnt = (list_n + gridDim.x - 1u) / gridDim.x;
+                    cnt = cnt > 64u ? 64u : cnt;
+                    bt = atomicAdd(counter, cnt);
                 } else {
                     const uint32_t cur = __hip_atomic_load(counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     const uint32_t rem = cur < Q.units ? Q.units - cur : 0u;
@@ -1932,7 +1940,7 @@ RT_DEV bool take_sample(ItemPool& pool, bool want, const DevCamera& C, const Dev
             }
             pool.batch = bt;
             pool.next = list ? bt : 0u;
-            pool.end = list ? (bt + 64u < list_n ? bt + 64u : list_n) : 64u * cnt;
+            pool.end = list ? (bt + cnt < list_n ? bt + cnt : list_n) : 64u * cnt;
             continue;
         }
         uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
@@ -2178,6 +2186,9 @@ __global__ __launch_bounds__(64, kWaves) void trace_samples(DevScene Sg, DevCame
     Ray ray{};
     ItemPool pool{0u, 0u, 0u, false};
     PROF_INIT();
+#ifdef RT_PROFILE_REGIONS
+    const unsigned long long wave_t0 = __builtin_amdgcn_s_memrealtime();
+#endif
     if constexpr (kKind == 0 && (kF & kFSusp) != 0u) {  // the suspending walk (world_walk)
         Walk w{};
         w.pos = 0u;
@@ -2283,6 +2294,12 @@ __global__ __launch_bounds__(64, kWaves) void trace_samples(DevScene Sg, DevCame
         }
     }
     PROF_FLUSH();
+#ifdef RT_PROFILE_REGIONS
+    if (kKind == 0 && lane == 0u && blockIdx.x < kProfWaves) {
+        g_wave_t[2u * blockIdx.x] = wave_t0;
+        g_wave_t[2u * blockIdx.x + 1u] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
 }
 
 // color_accumulator += ray_color(...) in sample order, then / spp (renderer.rs:140-147).
@@ -2709,6 +2726,29 @@ int rt_scene_free(rt_scene_handle s) {
                             "[%llu,%llu,%llu,%llu,%llu,%llu,%llu,%llu]}\n",
                     th[0], th[1], th[2], th[3], th[4], th[5], th[6], th[7], th[8], th[9], th[10], th[11], th[12],
                     th[13], th[14], th[15]);
+        }
+        {
+            static unsigned long long wt[2 * kProfWaves];
+            if (hipMemcpyFromSymbol(wt, HIP_SYMBOL(g_wave_t), sizeof wt) == hipSuccess) {
+                std::vector<unsigned long long> st, en;
+                for (uint32_t i = 0; i < kProfWaves; ++i)
+                    if (wt[2 * i + 1]) {
+                        st.push_back(wt[2 * i]);
+                        en.push_back(wt[2 * i + 1]);
+                    }
+                if (!st.empty()) {
+                    std::sort(st.begin(), st.end());
+                    std::sort(en.begin(), en.end());
+                    const unsigned long long t0 = st.front();
+                    auto q = [&](const std::vector<unsigned long long>& v, double f) {
+                        return (double)(v[(size_t)(f * (double)(v.size() - 1))] - t0) / 100.0;  // 100 MHz -> us
+                    };
+                    fprintf(stderr, "{\"wave_times_us\": {\"waves\": %zu, \"start\": [%.1f, %.1f, %.1f], "
+                                    "\"end\": [%.1f, %.1f, %.1f, %.1f, %.1f]}}\n",
+                            st.size(), q(st, 0.5), q(st, 0.99), q(st, 1.0), q(en, 0.0), q(en, 0.1), q(en, 0.5),
+                            q(en, 0.9), q(en, 1.0));
+                }
+            }
         }
 #endif
 #ifdef RT_LEAF_AUDIT

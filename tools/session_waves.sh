@@ -1,0 +1,6 @@
+set -u
+mkdir -p gpurun_out/waves; export TMPDIR=/tmp
+O=gpurun_out/waves
+L=raytracinginoneweekendinrust_amd/_lib
+for spp in 63 500; do RT_LIBRARY=$L/librtamd_prof.so timeout -k 10 200 python3 tools/region_profile.py --config C3 --spp $spp > $O/c3_$spp.log 2>&1 || exit 1; grep -E "wave_times|trace" $O/c3_$spp.log; done
+timeout -k 10 600 python -u -m pytest tests/test_gpu_multiprocess.py -q -x --timeout 500 --timeout-method thread > $O/mp_test.log 2>&1; echo "mp test rc=$?"; tail -3 $O/mp_test.log
