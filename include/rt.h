@@ -275,6 +275,8 @@ int rt_bvh_build_order(const float* d_keys, uint32_t n, uint64_t seed, uint32_t*
  *   RT_OPT_LAUNCH_LOG       1 = print the launched kernel instance and replay counts on stderr
  *   RT_OPT_BVH_BUILD        leaf ordering of BVHs at upload: 0 = device for >= 16384 items
  *                           (default), 1 = host always, 2 = device always
+ *   RT_OPT_GUIDE            guided batch divisor K: a batch is at most (units left) /
+ *                           (K x waves) units (1..256; 0 = the default 2)
  * Returns RT_ERR_INVALID for an unknown option or a value out of range. */
 typedef enum {
     RT_OPT_TUNE = 0,
@@ -284,7 +286,8 @@ typedef enum {
     RT_OPT_HRPP_SLOT_BITS = 4,
     RT_OPT_LAUNCH_LOG = 5,
     RT_OPT_BVH_BUILD = 6,
-    RT_OPT_COUNT = 7
+    RT_OPT_GUIDE = 7,
+    RT_OPT_COUNT = 8
 } rt_option;
 int rt_set_option(int option, int64_t value);
 int rt_get_option(int option, int64_t* value);

@@ -89,6 +89,9 @@ __device__ unsigned long long g_prof[kProfCopies * kProfWords];
 // ramp at the start and the drain at the end of a launch (tools/region_profile.py --waves)
 constexpr uint32_t kProfWaves = 8192;
 __device__ unsigned long long g_wave_t[2 * kProfWaves];
+// segments executed per 200 us since each wave's start (the fast kernel's throughput over a launch)
+constexpr uint32_t kTpBuckets = 4096, kTpTicks = 20000u;  // s_memrealtime ticks (100 MHz) per bucket
+__device__ unsigned long long g_tp_hist[kTpBuckets];
 __shared__ unsigned long long prof_lds[kProfWords];
 // per-traversal node-visit histograms (prof_lds[3 * kPrCount + bin]: lanes,
 // [3 * kPrCount + 8 + bin]: the wave's max per call); bins 0,1,2,3-4,5-8,9-16,17-32,33+
@@ -1766,7 +1769,7 @@ struct ChunkParams {
     uint32_t sample0;         // global sample index of chunk sample 0 (includes P.sample_base)
     uint32_t samples;         // samples per pixel in this chunk
     uint32_t units;           // work units: (8x8 block of the shard, sample) pairs, block-major
-    uint32_t pad;
+    uint32_t guide;           // the guided batch divisor: a batch is at most rem / (guide x waves) units
     uint32_t nslots;          // sample-buffer plane size: 64 slots per 8x8 block of the shard, block-major
     uint32_t group;           // units per batch at most (batch_group)
 };
@@ -1927,7 +1930,7 @@ RT_DEV bool take_sample(ItemPool& pool, bool want, const DevCamera& C, const Dev
                 } else {
                     const uint32_t cur = __hip_atomic_load(counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     const uint32_t rem = cur < Q.units ? Q.units - cur : 0u;
-                    cnt = rem / (2u * gridDim.x);
+                    cnt = rem / (Q.guide * gridDim.x);
                     cnt = cnt < 1u ? 1u : (cnt > Q.group ? Q.group : cnt);
                     bt = atomicAdd(counter, cnt);
                 }
@@ -2188,6 +2191,7 @@ __global__ __launch_bounds__(64, kWaves) void trace_samples(DevScene Sg, DevCame
     PROF_INIT();
 #ifdef RT_PROFILE_REGIONS
     const unsigned long long wave_t0 = __builtin_amdgcn_s_memrealtime();
+    uint32_t tp_bucket = 0u, tp_acc = 0u;
 #endif
     if constexpr (kKind == 0 && (kF & kFSusp) != 0u) {  // the suspending walk (world_walk)
         Walk w{};
@@ -2241,6 +2245,17 @@ __global__ __launch_bounds__(64, kWaves) void trace_samples(DevScene Sg, DevCame
         }
         PROF_ADD(kPrRefill, pr);
         if (__ballot(has) == 0ull) break;  // pool exhausted and every path finished
+#ifdef RT_PROFILE_REGIONS
+        if (kKind == 0) {  // throughput histogram: this iteration's segments into the current bucket
+            const uint32_t b = (uint32_t)((__builtin_amdgcn_s_memrealtime() - wave_t0) / kTpTicks);
+            if (b != tp_bucket) {
+                if (lane == 0u && tp_acc && tp_bucket < kTpBuckets) atomicAdd(&g_tp_hist[tp_bucket], tp_acc);
+                tp_bucket = b;
+                tp_acc = 0u;
+            }
+            tp_acc += (uint32_t)__popcll(__ballot(has));
+        }
+#endif
         if constexpr ((kF & kFMarble) != 0u) {
             bool shade = false, any = false;
             float t = 0.0f;
@@ -2295,6 +2310,7 @@ __global__ __launch_bounds__(64, kWaves) void trace_samples(DevScene Sg, DevCame
     }
     PROF_FLUSH();
 #ifdef RT_PROFILE_REGIONS
+    if (kKind == 0 && lane == 0u && tp_acc && tp_bucket < kTpBuckets) atomicAdd(&g_tp_hist[tp_bucket], tp_acc);
     if (kKind == 0 && lane == 0u && blockIdx.x < kProfWaves) {
         g_wave_t[2u * blockIdx.x] = wave_t0;
         g_wave_t[2u * blockIdx.x + 1u] = __builtin_amdgcn_s_memrealtime();
@@ -2538,7 +2554,7 @@ TraceKernel fast_instance(int waves, uint32_t features) {
 }
 
 // rt_set_option's process-wide diagnostic switches (include/rt.h rt_option).
-std::atomic<int64_t> g_opt[RT_OPT_COUNT] = {{0}, {0}, {0}, {0}, {-1}, {0}, {0}};
+std::atomic<int64_t> g_opt[RT_OPT_COUNT] = {{0}, {0}, {0}, {0}, {-1}, {0}, {0}, {0}};
 int64_t opt(int o) { return g_opt[o].load(std::memory_order_relaxed); }
 
 int check_device(int device) {
@@ -2748,6 +2764,15 @@ int rt_scene_free(rt_scene_handle s) {
                             st.size(), q(st, 0.5), q(st, 0.99), q(st, 1.0), q(en, 0.0), q(en, 0.1), q(en, 0.5),
                             q(en, 0.9), q(en, 1.0));
                 }
+            }
+            static unsigned long long tp[kTpBuckets];
+            if (hipMemcpyFromSymbol(tp, HIP_SYMBOL(g_tp_hist), sizeof tp) == hipSuccess) {
+                uint32_t n = kTpBuckets;
+                while (n > 0u && tp[n - 1u] == 0u) --n;
+                fprintf(stderr, "{\"tp_gseg_per_s\": {\"bucket_us\": %u, \"rate\": [", kTpTicks / 100u);
+                for (uint32_t i = 0; i < n; ++i)  // segments per bucket -> G segments / s
+                    fprintf(stderr, "%s%.3f", i ? "," : "", (double)tp[i] / (kTpTicks * 10.0));
+                fprintf(stderr, "]}}\n");
             }
         }
 #endif
@@ -3030,7 +3055,8 @@ int rt_render_launch_camera(rt_scene_handle s, const rt_camera* camera, const rt
         q.group = batch_group(q.units, exact || dev_ref.hrpp_tab ? (uint32_t)s->grid_ref : (uint32_t)s->grid);
         if (const int64_t gr = opt(RT_OPT_GROUP)) q.group = (uint32_t)gr;  // diagnostics / A-B runs
         if (q.group > q.samples) q.group = q.samples;  // a batch crosses at most one block boundary
-        q.pad = 0u;
+        q.guide = 2u;  // measured on C3 (63 and 500 spp): 2 beats 4, 8, 16 and 32 (tools/session_guide.sh)
+        if (const int64_t gd = opt(RT_OPT_GUIDE)) q.guide = (uint32_t)gd;  // diagnostics / A-B runs
         q.nslots = (uint32_t)nslots;
         if ((e = hipMemsetAsync(s->counter, 0, sizeof(TraceCounters), st)) != hipSuccess)
             return hip_fail(e, "memset counters");
@@ -3271,6 +3297,7 @@ int rt_set_option(int option, int64_t value) {
         case RT_OPT_HRPP_SLOT_BITS: ok = value >= -1 && value <= 28; break;
         case RT_OPT_LAUNCH_LOG: ok = value == 0 || value == 1; break;
         case RT_OPT_BVH_BUILD: ok = value >= 0 && value <= 2; break;
+        case RT_OPT_GUIDE: ok = value >= 0 && value <= 256; break;
     }
     if (!ok) return rthost::set_error(RT_ERR_INVALID, "option value out of range");
     g_opt[option].store(value, std::memory_order_relaxed);

@@ -149,10 +149,14 @@ def test_diagnostic_options_are_explicit(rt):
         if f.endswith((".hip", ".cpp", ".hpp")):
             assert "getenv" not in open(os.path.join(csrc, f)).read(), f
     assert rt.get_option("tune") == 0 and rt.get_option("hrpp_slot_bits") == -1
+    with rt.options(guide=8):
+        assert rt.get_option("guide") == 8
+    assert rt.get_option("guide") == 0
     with rt.options(tune=1 << 16, stack_lds=2, bvh_build=1):
         assert (rt.get_option("tune"), rt.get_option("stack_lds"), rt.get_option("bvh_build")) == (1 << 16, 2, 1)
     assert (rt.get_option("tune"), rt.get_option("stack_lds"), rt.get_option("bvh_build")) == (0, 0, 0)
-    for name, bad in (("group", 65), ("launch_log", 2), ("hrpp_slot_bits", 29), ("bvh_build", 3), ("stack_lds", -1)):
+    for name, bad in (("group", 65), ("launch_log", 2), ("hrpp_slot_bits", 29), ("bvh_build", 3), ("stack_lds", -1),
+                      ("guide", 257)):
         with pytest.raises(rt.RTError, match="RT_ERR_INVALID"):
             rt.set_option(name, bad)
     assert _capi.lib.rt_set_option(99, 0) == -1

@@ -34,6 +34,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="C3")
     ap.add_argument("--spp", type=int, default=None)
+    ap.add_argument("--shard", type=int, default=1, help="render shard 0 of N (bench.py's block interleave)")
     args = ap.parse_args()
     if not any(k in os.environ.get("RT_LIBRARY", "") for k in ("_prof", "_audit")):
         sys.exit("set RT_LIBRARY to the _prof or _audit build")
@@ -47,7 +48,8 @@ def main():
         cfg = cfg.scaled(cfg.width, args.spp)
     scene = rt.Scene.generate(cfg.scene, cfg.scene_seed)
     ds = rt.DeviceScene(scene)
-    p = rt.render_params(cfg.width, cfg.height, cfg.spp, cfg.depth, background=cfg.background(), seed=cfg.render_seed)
+    p = rt.render_params(cfg.width, cfg.height, cfg.spp, cfg.depth, background=cfg.background(), seed=cfg.render_seed,
+                         shard_index=0, shard_count=args.shard)
     out = torch.zeros(cfg.width * cfg.height * 3, dtype=torch.float32, device="cuda")
     seg = torch.zeros(1, dtype=torch.int64, device="cuda")
     ds.launch(cfg.camera(), p, out.data_ptr(), seg.data_ptr(), 0)
@@ -65,14 +67,14 @@ def main():
         captured = tf.read().splitlines()
         lines = [ln for ln in captured if ln.startswith('{"rt_profile"')]
         for ln in captured:
-            if ln.startswith(('{"leaf_audit', '{"audit', '{"trav_audit', '{"bounds_audit', '{"trips_hist', '{"wave_times')):
+            if ln.startswith(('{"leaf_audit', '{"audit', '{"trav_audit', '{"bounds_audit', '{"trips_hist', '{"wave_times', '{"tp_gseg')):
                 print(ln)
     if not lines:  # an audit build: no region counters
         return
     v = json.loads(lines[-1])["rt_profile"]
     cyc, cnt, lanes = v[:COUNT], v[COUNT:2 * COUNT], v[2 * COUNT:]
     total = cyc[0] + cyc[1] + cyc[2]  # refill + finish_segment + world_hit: the whole loop
-    samples = cfg.width * cfg.height * cfg.spp
+    samples = cfg.width * cfg.height * cfg.spp // args.shard
     print(f"{cfg.name} {cfg.width}x{cfg.height} {cfg.spp}spp: trace {ms:.1f} ms, {segments} segments, "
           f"{segments / samples:.3f} seg/sample, wave cycles refill+segment = {total:.4g}")
     rows = []

@@ -19,6 +19,7 @@ def main():
     ap.add_argument("--n", type=int, default=8)
     ap.add_argument("--rank", type=int, default=0)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--spp", type=int, default=None, help="override the config's samples per pixel")
     a = ap.parse_args()
     import torch
     import raytracinginoneweekendinrust_amd as rt
@@ -26,6 +27,8 @@ def main():
     import rtopts
     rtopts.apply(rt)  # RT_GROUP=... of the session scripts
     cfg = rt.CONFIGS[a.config]
+    if a.spp:
+        cfg = cfg.scaled(cfg.width, a.spp)
     scene = rt.Scene.generate(cfg.scene, cfg.scene_seed)
     ds = rt.DeviceScene(scene)
     out = torch.zeros(cfg.width * cfg.height * 3, dtype=torch.float32, device="cuda")
