@@ -68,6 +68,9 @@ enum ProfRegion : uint32_t {
 // from DevParams::tune (rt_set_option(RT_OPT_TUNE), diagnostics / A-B runs).
 constexpr uint32_t kModeExact = 1u, kModeNoLeafBoxes = 2u, kModeNoPermLds = 32u, kModeW3 = 64u,
                    kModeNoPretest = 128u, kModeReplayRef = 1u << 16;  // ReplayRef: the replay pass runs trace_samples<1>
+// NoStream: no streaming replay pass beside the fast kernel (the serialized pass takes every
+// handed-over sample after it); the tests cover both
+constexpr uint32_t kModeNoStream = 1u << 17;
 // EXPERIMENT ONLY (RT_OPT_TUNE, not exact): closest-hit pruning also on BVHs the proof does not
 // cover (triangles, moving spheres), to measure what an exact bound for them could gain.
 constexpr uint32_t kModePruneAllExp = 1u << 20;
@@ -92,6 +95,17 @@ __device__ unsigned long long g_wave_t[2 * kProfWaves];
 // segments executed per 200 us since each wave's start (the fast kernel's throughput over a launch)
 constexpr uint32_t kTpBuckets = 4096, kTpTicks = 20000u;  // s_memrealtime ticks (100 MHz) per bucket
 __device__ unsigned long long g_tp_hist[kTpBuckets];
+// streaming replay pass events: (s_memrealtime, claimed entry or ~0 at the wave's exit)
+constexpr uint32_t kRoleEvents = 4096;
+__device__ unsigned long long g_role_ev[2 * kRoleEvents];
+__device__ unsigned g_role_n;
+__device__ __forceinline__ void role_event(uint32_t what) {
+    const unsigned i = atomicAdd(&g_role_n, 1u);
+    if (i < kRoleEvents) {
+        g_role_ev[2u * i] = __builtin_amdgcn_s_memrealtime();
+        g_role_ev[2u * i + 1u] = what;
+    }
+}
 __shared__ unsigned long long prof_lds[kProfWords];
 // per-traversal node-visit histograms (prof_lds[3 * kPrCount + bin]: lanes,
 // [3 * kPrCount + 8 + bin]: the wave's max per call); bins 0,1,2,3-4,5-8,9-16,17-32,33+
@@ -1770,6 +1784,7 @@ struct ChunkParams {
     uint32_t samples;         // samples per pixel in this chunk
     uint32_t units;           // work units: (8x8 block of the shard, sample) pairs, block-major
     uint32_t guide;           // the guided batch divisor: a batch is at most rem / (guide x waves) units
+    uint32_t fast_grid;       // waves of the fast kernel's launch (the streaming replay pass waits for them)
     uint32_t nslots;          // sample-buffer plane size: 64 slots per 8x8 block of the shard, block-major
     uint32_t group;           // units per batch at most (batch_group)
 };
@@ -1897,12 +1912,63 @@ struct TraceCounters {
     unsigned replay_count;       // samples handed to the reference kernel
     unsigned replay_pull;        // next replay-list entry (reference kernel)
     unsigned batch_full;         // next batch when the replay list overflowed
-    unsigned long long fast_segments;  // segments of the fast kernel's completed samples
+    unsigned fast_done;          // fast-kernel waves that have finished (the streaming replay's end)
+    unsigned stream_abort;       // the streaming replay gave up a claimed entry: re-render the chunk
+    unsigned long long fast_segments;  // segments of the fast kernel's and streaming replay's samples
 };
-// A replay-list entry: the sample's pixel and its chunk-local sample index.
+// A replay-list entry: the sample's pixel and its chunk-local sample index. Entries are
+// written and read as one 64-bit agent-scope atomic: the streaming replay pass reads them
+// while the fast kernel still runs, on other XCDs. A free entry holds kReplayFree.
 struct ReplayItem {
     uint32_t pixel, sample;
 };
+constexpr unsigned long long kReplayFree = ~0ull;
+RT_DEV void replay_publish(ReplayItem* list, uint32_t idx, uint32_t pixel, uint32_t sample) {
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(list + idx),
+                       (unsigned long long)pixel | ((unsigned long long)sample << 32), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+RT_DEV unsigned long long replay_peek(const ReplayItem* list, uint32_t idx) {
+    return __hip_atomic_load(reinterpret_cast<const unsigned long long*>(list + idx), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+}
+// Takes entry idx and frees it for the next chunk.
+RT_DEV ReplayItem replay_take(const ReplayItem* list, uint32_t idx) {
+    const unsigned long long v = replay_peek(list, idx);
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(const_cast<ReplayItem*>(list) + idx), kReplayFree,
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return ReplayItem{(uint32_t)v, (uint32_t)(v >> 32)};
+}
+constexpr uint32_t kReplayCap = 1u << 20;
+// The streaming replay pass (trace_samples<3> with fixup 2, on a second stream) claims
+// entries one at a time while the fast kernel drains. Returns the claimed entry's index once
+// it is published, or kReplayNone when the fast kernel finished without one, the list
+// overflowed, or the wait timed out (then the serialized pass re-renders the chunk).
+constexpr uint32_t kReplayNone = 0xffffffffu;
+constexpr uint32_t kStreamWaves = 512;  // waves of the streaming replay pass
+constexpr unsigned long long kStreamTimeoutTicks = 1000000000ull;  // 10 s of s_memrealtime (100 MHz)
+RT_DEV uint32_t replay_claim(TraceCounters* ctr, const ReplayItem* list, uint32_t fast_grid) {
+    const uint32_t i = atomicAdd(&ctr->replay_pull, 1u);
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+        // fast_done first: once every fast wave has counted itself out (after a release
+        // fence), replay_count is final
+        const bool done = __hip_atomic_load(&ctr->fast_done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) >= fast_grid;
+        const uint32_t n = __hip_atomic_load(&ctr->replay_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (i < n) {
+            if (i >= kReplayCap) return kReplayNone;
+            if (replay_peek(list, i) != kReplayFree) return i;
+        } else if (done) {
+            return kReplayNone;
+        }
+        if (__builtin_amdgcn_s_memrealtime() - t0 > kStreamTimeoutTicks) {
+            atomicExch(&ctr->stream_abort, 1u);
+            return kReplayNone;
+        }
+        for (int z = 0; z < 4; ++z)  // ~32k cycles between polls: the pollers must not crowd the drain
+            __builtin_amdgcn_s_sleep(127);
+    }
+}
 // Gives the next work item to every lane with `want` set. A lane that got a
 // sample returns true with its camera ray started (renderer.rs:141-143); a
 // max_depth 0 sample (ray.rs:39-41: black, no segment) is stored and skipped.
@@ -1910,7 +1976,8 @@ struct ReplayItem {
 // through *counter in shares of ceil(list_n / waves), at most 64: the replayed
 // paths are few and long, and a wave's segment takes as long as its slowest lane).
 RT_DEV bool take_sample(ItemPool& pool, bool want, const DevCamera& C, const DevParams& P, const ChunkParams& Q,
-                        const Key& k, unsigned* counter, const ReplayItem* list, uint32_t list_n, float* sbuf,
+                        const Key& k, unsigned* counter, const ReplayItem* list, uint32_t list_n,
+                        TraceCounters* ctr, uint32_t stream_grid, float* sbuf,
                         uint32_t lane, uint32_t& slot, uint32_t& s_local, V& L, V& T, uint32_t& depth, Rng& g,
                         Ray& ray) {
     bool got = false;
@@ -1922,8 +1989,27 @@ RT_DEV bool take_sample(ItemPool& pool, bool want, const DevCamera& C, const Dev
             // work left (rem / (2 x waves), at least one unit) so that the waves finish together
             // instead of the last ones draining a full batch alone.
             uint32_t bt = 0, cnt = 64u;
+            if (list && stream_grid) {
+                // The streaming replay keeps 1 + backlog / waves lanes of a wave busy: the
+                // replayed paths are few and long, and a wave's segment takes as long as its
+                // slowest lane, so they spread over the waves unless there are many.
+                uint32_t lim = 1u;
+                if (lane == 0u) {
+                    const uint32_t n = __hip_atomic_load(&ctr->replay_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const uint32_t pl = __hip_atomic_load(&ctr->replay_pull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    lim += (n > pl ? n - pl : 0u) / gridDim.x;
+                }
+                lim = __builtin_amdgcn_readfirstlane(lim);
+                if (64u - (uint32_t)__popcll(need) >= lim) break;
+            }
             if (lane == 0u) {
-                if (list) {  // a share of the list per wave: a replayed path runs with few others
+                if (list && stream_grid) {  // the streaming replay: one entry per claim
+                    cnt = 1u;
+                    bt = replay_claim(ctr, list, stream_grid);
+#ifdef RT_PROFILE_REGIONS
+                    role_event(bt);
+#endif
+                } else if (list) {  // a share of the list per wave: a replayed path runs with few others
                     cnt = (list_n + gridDim.x - 1u) / gridDim.x;
                     cnt = cnt > 64u ? 64u : cnt;
                     bt = atomicAdd(counter, cnt);
@@ -1951,7 +2037,7 @@ RT_DEV bool take_sample(ItemPool& pool, bool want, const DevCamera& C, const Dev
         if (want && !got && rank < avail) {
             uint32_t x, y, s, sl;
             if (list) {
-                const ReplayItem it = list[pool.next + rank];
+                const ReplayItem it = replay_take(list, pool.next + rank);
                 y = it.pixel / P.width;
                 x = it.pixel - y * P.width;
                 s = it.sample;
@@ -2126,7 +2212,6 @@ RT_DEV bool shade_marble(const DevScene& S, const DevParams& P, const ChunkParam
 // re-traced sample is exactly the reference's. Should the list overflow, the
 // fixup kernel re-renders the whole chunk and takes back the fast kernel's
 // segment count.
-constexpr uint32_t kReplayCap = 1u << 20;
 #ifndef RT_SUSPEND
 #define RT_SUSPEND 16
 #endif
@@ -2164,16 +2249,28 @@ __global__ __launch_bounds__(64, kWaves) void trace_samples(DevScene Sg, DevCame
     // item source: the chunk's block batches, or (fixup) the replay list
     unsigned* counter = &ctr->batch;
     const ReplayItem* list = nullptr;
-    uint32_t list_n = 0u;
-    if ((kKind == 1 || kKind == 3) && fixup) {
+    uint32_t list_n = 0u, stream_grid = 0u;
+    if ((kKind == 1 || kKind == 3) && fixup == 2u) {
+        // The streaming replay pass, beside the fast kernel on a second stream: its waves take
+        // the slots the fast kernel's waves leave as it drains. One dispatched while the fast
+        // kernel still has work gives its slot back at once.
+        if (__hip_atomic_load(&ctr->batch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < Q.units) return;
+        list = replay_list;
+        list_n = kReplayCap;
+        counter = &ctr->replay_pull;
+        stream_grid = Q.fast_grid;
+    } else if ((kKind == 1 || kKind == 3) && fixup) {
         const uint32_t n = __hip_atomic_load(&ctr->replay_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (n <= kReplayCap) {
+        const bool abort = __hip_atomic_load(&ctr->stream_abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+        if (n <= kReplayCap && !abort) {  // the entries the streaming pass (if any) did not take
             if (n == 0u) return;
             list = replay_list;
             list_n = n;
             counter = &ctr->replay_pull;
-        } else {  // overflow: re-render the chunk; its segments replace the fast kernel's
+        } else {  // overflow: re-render the chunk; its segments replace the earlier passes'
             counter = &ctr->batch_full;
+            for (uint32_t i = blockIdx.x * 64u + lane; i < kReplayCap; i += gridDim.x * 64u)
+                (void)replay_take(replay_list, i);  // free the list for the next chunk
             if (blockIdx.x == 0u && lane == 0u && seg_counter)
                 atomicAdd(seg_counter, 0ull - __hip_atomic_load(&ctr->fast_segments, __ATOMIC_RELAXED,
                                                                 __HIP_MEMORY_SCOPE_AGENT));
@@ -2198,7 +2295,7 @@ __global__ __launch_bounds__(64, kWaves) void trace_samples(DevScene Sg, DevCame
         w.pos = 0u;
         for (;;) {
             PROF_T0(pr);
-            if (take_sample(pool, !has, C, P, Q, k, counter, list, list_n, sbuf, lane, slot, take_sample_idx, L, T, depth, g,
+            if (take_sample(pool, !has, C, P, Q, k, counter, list, list_n, ctr, stream_grid, sbuf, lane, slot, take_sample_idx, L, T, depth, g,
                             ray)) {
                 has = true;
                 nseg_sample = 0;
@@ -2218,7 +2315,7 @@ __global__ __launch_bounds__(64, kWaves) void trace_samples(DevScene Sg, DevCame
             PROF_ADD(kPrWorld, pw);
             if (has && replay) {  // hand the sample to the reference kernel
                 unsigned idx = atomicAdd(&ctr->replay_count, 1u);
-                if (idx < kReplayCap) replay_list[idx] = ReplayItem{g.pixel, g.sample - Q.sample0};
+                if (idx < kReplayCap) replay_publish(replay_list, idx, g.pixel, g.sample - Q.sample0);
                 has = false;
             }
             const bool walked = has && w.pos == S.num_top;
@@ -2238,7 +2335,7 @@ __global__ __launch_bounds__(64, kWaves) void trace_samples(DevScene Sg, DevCame
     } else
     for (;;) {
         PROF_T0(pr);
-        if (take_sample(pool, !has, C, P, Q, k, counter, list, list_n, sbuf, lane, slot, take_sample_idx, L, T, depth, g,
+        if (take_sample(pool, !has, C, P, Q, k, counter, list, list_n, ctr, stream_grid, sbuf, lane, slot, take_sample_idx, L, T, depth, g,
                         ray)) {
             has = true;
             nseg_sample = 0;
@@ -2268,7 +2365,7 @@ __global__ __launch_bounds__(64, kWaves) void trace_samples(DevScene Sg, DevCame
                 PROF_ADD(kPrWorld, pw);
                 if (kKind == 0 && replay) {  // hand the sample to the reference kernel
                     unsigned idx = atomicAdd(&ctr->replay_count, 1u);
-                    if (idx < kReplayCap) replay_list[idx] = ReplayItem{g.pixel, g.sample - Q.sample0};
+                    if (idx < kReplayCap) replay_publish(replay_list, idx, g.pixel, g.sample - Q.sample0);
                     has = false;
                 } else {
                     shade = true;
@@ -2288,7 +2385,7 @@ __global__ __launch_bounds__(64, kWaves) void trace_samples(DevScene Sg, DevCame
             PROF_ADD(kPrWorld, pw);
             if (kKind == 0 && replay) {  // hand the sample to the reference kernel
                 unsigned idx = atomicAdd(&ctr->replay_count, 1u);
-                if (idx < kReplayCap) replay_list[idx] = ReplayItem{g.pixel, g.sample - Q.sample0};
+                if (idx < kReplayCap) replay_publish(replay_list, idx, g.pixel, g.sample - Q.sample0);
                 has = false;
             } else if (finish_segment<kF>(S, P, Q, k, sbuf, any, he, hc, t, ray, L, T, depth, g, slot, g.sample - Q.sample0)) {
                 has = false;
@@ -2305,12 +2402,17 @@ __global__ __launch_bounds__(64, kWaves) void trace_samples(DevScene Sg, DevCame
         for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
         if (lane == 0u) {
             atomicAdd(seg_counter, v);
-            if (kKind == 0) atomicAdd(&ctr->fast_segments, v);
+            if (kKind == 0 || stream_grid) atomicAdd(&ctr->fast_segments, v);
         }
+    }
+    if (kKind == 0 && lane == 0u) {  // count the wave out for the streaming replay pass
+        __threadfence();  // (release: its replay-list entries and replay_count increments first)
+        atomicAdd(&ctr->fast_done, 1u);
     }
     PROF_FLUSH();
 #ifdef RT_PROFILE_REGIONS
     if (kKind == 0 && lane == 0u && tp_acc && tp_bucket < kTpBuckets) atomicAdd(&g_tp_hist[tp_bucket], tp_acc);
+    if (stream_grid && lane == 0u) role_event(0xfffffffeu);
     if (kKind == 0 && lane == 0u && blockIdx.x < kProfWaves) {
         g_wave_t[2u * blockIdx.x] = wave_t0;
         g_wave_t[2u * blockIdx.x + 1u] = __builtin_amdgcn_s_memrealtime();
@@ -2475,7 +2577,10 @@ struct rt_scene {
     int fast_waves = 0;          // 3 or 4: the trace_samples<0, kWaves, kF> instance this scene launches
     uint32_t features = kFAll;   // kF bits the scene needs (BVHs, triangles, long sphere runs, deep stacks)
     uint32_t* stack_spill = nullptr;  // kFDeep: HBM stack entries past kStackLdsMax, grid x spill_depth x 64 x 2 words
-    ReplayItem* replay = nullptr;  // kReplayCap entries
+    ReplayItem* replay = nullptr;  // kReplayCap entries, kReplayFree between chunks
+    // the streaming replay pass runs on `aux`, forked from and joined back into the launch's stream
+    hipStream_t aux = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
     float coord_bound = 0.0f;
     // HRPP experiment: tables (allocated at the first RT_FLAG_HRPP render) and counters
     rtdev::HrppSlot* hrpp_tab = nullptr;
@@ -2765,6 +2870,19 @@ int rt_scene_free(rt_scene_handle s) {
                             q(en, 0.9), q(en, 1.0));
                 }
             }
+            static unsigned long long rv[2 * kRoleEvents];
+            unsigned rn = 0;
+            if (hipMemcpyFromSymbol(&rn, HIP_SYMBOL(g_role_n), sizeof rn) == hipSuccess && rn &&
+                hipMemcpyFromSymbol(rv, HIP_SYMBOL(g_role_ev), sizeof rv) == hipSuccess) {
+                unsigned long long t0 = ~0ull;
+                for (uint32_t i = 0; i < kProfWaves; ++i)
+                    if (wt[2 * i + 1] && wt[2 * i] < t0) t0 = wt[2 * i];
+                fprintf(stderr, "{\"role_events_us\": [");
+                for (unsigned i = 0; i < rn && i < kRoleEvents; ++i)
+                    fprintf(stderr, "%s[%.1f, %lld]", i ? "," : "", ((double)rv[2 * i] - (double)t0) / 100.0,
+                            rv[2 * i + 1] >= 0xfffffffeull ? -(long long)(rv[2 * i + 1] - 0xfffffffdull) : (long long)rv[2 * i + 1]);
+                fprintf(stderr, "]}\n");
+            }
             static unsigned long long tp[kTpBuckets];
             if (hipMemcpyFromSymbol(tp, HIP_SYMBOL(g_tp_hist), sizeof tp) == hipSuccess) {
                 uint32_t n = kTpBuckets;
@@ -2811,6 +2929,9 @@ int rt_scene_free(rt_scene_handle s) {
         if (s->counter) (void)hipFree(s->counter);
         if (s->stack_spill) (void)hipFree(s->stack_spill);
         if (s->replay) (void)hipFree(s->replay);
+        if (s->fork) (void)hipEventDestroy(s->fork);
+        if (s->join) (void)hipEventDestroy(s->join);
+        if (s->aux) (void)hipStreamDestroy(s->aux);
         if (s->hrpp_tab) (void)hipFree(s->hrpp_tab);
         if (s->hrpp_stats) (void)hipFree(s->hrpp_stats);
         for (int i = 0; i < rt_scene::kEvents; ++i)
@@ -2976,6 +3097,18 @@ int rt_render_launch_camera(rt_scene_handle s, const rt_camera* camera, const rt
     if (!s->replay) {
         if ((e = hipMalloc(&s->replay, sizeof(ReplayItem) * (size_t)kReplayCap)) != hipSuccess)
             return rthost::set_error(RT_ERR_OOM, std::string("hipMalloc replay list: ") + hipGetErrorString(e));
+        if ((e = hipMemsetAsync(s->replay, 0xff, sizeof(ReplayItem) * (size_t)kReplayCap, (hipStream_t)stream)) !=
+            hipSuccess)  // every entry kReplayFree
+            return hip_fail(e, "replay list reset");
+    }
+    if (!s->aux) {
+        if ((e = hipStreamCreateWithFlags(&s->aux, hipStreamNonBlocking)) != hipSuccess) {
+            s->aux = nullptr;
+            return hip_fail(e, "hipStreamCreate (replay stream)");
+        }
+        if ((e = hipEventCreateWithFlags(&s->fork, hipEventDisableTiming)) != hipSuccess ||
+            (e = hipEventCreateWithFlags(&s->join, hipEventDisableTiming)) != hipSuccess)
+            return hip_fail(e, "hipEventCreate (replay stream)");
     }
     // The fast kernel's instance: four waves per SIMD when that raises its occupancy
     // over three (the Perlin tables then stay in L2, so the stack alone sets LDS).
@@ -3063,6 +3196,7 @@ int rt_render_launch_camera(rt_scene_handle s, const rt_camera* camera, const rt
         uint32_t grid = (uint32_t)s->grid, grid_ref = (uint32_t)s->grid_ref;
         if (grid > q.units) grid = q.units;
         if (grid_ref > q.units) grid_ref = q.units;
+        q.fast_grid = grid;
         hipEvent_t* evp = nullptr;
         if (s->ev_count < rt_scene::kEvents) {
             evp = s->ev[s->ev_count];
@@ -3081,13 +3215,28 @@ int rt_render_launch_camera(rt_scene_handle s, const rt_camera* camera, const rt
                                s->sbuf, s->counter, s->replay, 0u, d_segments);
         } else {  // fast kernel, then the reference kernel on the samples it handed over
             const TraceKernel kf = fast_instance(s->fast_waves, s->features);
+            const bool kind3 = !(s->features & kFDeep) && !(dp.tune & kModeReplayRef);
+            const bool stream_rp = kind3 && !(dp.tune & kModeNoStream);
+            if (stream_rp && (e = hipEventRecord(s->fork, st)) != hipSuccess) return hip_fail(e, "replay stream fork");
             hipLaunchKernelGGL(kf, dim3(grid), dim3(64), lds, st, s->dev, cam, dp, q, s->sbuf, s->counter, s->replay,
                                0u, d_segments);
-            if (!(s->features & kFDeep) && !(dp.tune & kModeReplayRef)) {
+            if (kind3) {
                 // the replay pass: fast traversal except for the rays that were handed over
                 DevScene dev_rp = s->dev;
                 dev_rp.stack_depth = std::max(s->dev.stack_depth, s->stack_ref);
                 const size_t lds_rp = (size_t)dev_rp.stack_depth * 128u * sizeof(uint32_t) + perm_lds;
+                if (stream_rp) {  // streaming: takes the handed-over samples during the fast kernel's drain
+                    // few waves: each polls the counters while it waits (3072 pollers slowed the
+                    // drain they overlap by a third)
+                    const uint32_t grid_st = std::min(grid_ref, kStreamWaves);
+                    if ((e = hipStreamWaitEvent(s->aux, s->fork, 0)) != hipSuccess) return hip_fail(e, "replay stream wait");
+                    hipLaunchKernelGGL((trace_samples<3, 3, kFAll & ~kFDeep>), dim3(grid_st), dim3(64), lds_rp, s->aux,
+                                       dev_rp, cam, dp, q, s->sbuf, s->counter, s->replay, 2u, d_segments);
+                    if ((e = hipEventRecord(s->join, s->aux)) != hipSuccess ||
+                        (e = hipStreamWaitEvent(st, s->join, 0)) != hipSuccess)
+                        return hip_fail(e, "replay stream join");
+                }
+                // serialized: whatever the streaming pass did not take (everything without it)
                 hipLaunchKernelGGL((trace_samples<3, 3, kFAll & ~kFDeep>), dim3(grid_ref), dim3(64), lds_rp, st,
                                    dev_rp, cam, dp, q, s->sbuf, s->counter, s->replay, 1u, d_segments);
             } else {

@@ -377,3 +377,29 @@ def test_replay_pass_kernels_match_oracle(cfg_name, w, h, replay_ref, rt, orc):
         got, st = gpu_render(rt, scene, cam, params)
     np.testing.assert_array_equal(got, want)
     assert st["segments"] == cnt["segments"]
+
+
+@pytest.mark.parametrize("stream", [True, False])
+@pytest.mark.parametrize("cfg_name", ["C3", "C5"])
+def test_streaming_replay_pass_matches_oracle(cfg_name, stream, rt, orc):
+    # The streaming replay pass (kernel.hip replay_claim) runs beside the fast kernel and takes
+    # the handed-over samples while the fast kernel drains; RT_OPT_TUNE bit 17 leaves them all
+    # to the serialized pass. A 4096 x 1 image (v = j / (H - 1) = NaN: every ray is handed
+    # over) with 8 spp gives 4096 work units, enough to fill the GPU, so the fast kernel's
+    # waves drain while the stream's waves wait for slots, and every sample is replayed.
+    cfg = rt.CONFIGS[cfg_name]
+    scene = rt.Scene.generate(cfg.scene, cfg.scene_seed)
+    w, h, spp = 4096, 1, 8
+    cam = rt.Camera.new(cfg.look_from, cfg.look_at, cfg.view_up, cfg.vfov, w / h, cfg.aperture, cfg.focus_dist,
+                        cfg.time0, cfg.time1)
+    params = rt.render_params(w, h, spp, cfg.depth, background=cfg.background(), seed=9)
+    want, cnt = orc.render(scene, cam, params)
+    with rt.options(tune=0 if stream else 1 << 17):
+        ds = rt.DeviceScene(scene)
+        try:
+            for _ in range(2):  # the second render starts from the list the first one freed
+                got, st = ds.render(cam, params)
+                np.testing.assert_array_equal(got, want)
+                assert st["segments"] == cnt["segments"]
+        finally:
+            ds.close()

@@ -67,7 +67,7 @@ def main():
         captured = tf.read().splitlines()
         lines = [ln for ln in captured if ln.startswith('{"rt_profile"')]
         for ln in captured:
-            if ln.startswith(('{"leaf_audit', '{"audit', '{"trav_audit', '{"bounds_audit', '{"trips_hist', '{"wave_times', '{"tp_gseg')):
+            if ln.startswith(('{"leaf_audit', '{"audit', '{"trav_audit', '{"bounds_audit', '{"trips_hist', '{"wave_times', '{"tp_gseg', '{"role_ev')):
                 print(ln)
     if not lines:  # an audit build: no region counters
         return
