@@ -46,6 +46,13 @@ using rtdev::DevTexture;
 using rtdev::f4;
 
 #define RT_DEV __device__ __forceinline__
+// A/B diagnostic only (tools/session_*.sh variants): N wave-wide VALU instructions that do nothing,
+// to price issue slots at a point of the kernel (compiled out unless RT_PAD_* is defined).
+#define RT_VALU_PAD(N)                                                              \
+    do {                                                                            \
+        float _p = 0.0f;                                                            \
+        _Pragma("unroll") for (int _i = 0; _i < (N); ++_i) asm volatile("v_add_f32 %0, %0, %0" : "+v"(_p)); \
+    } while (0)
 
 namespace {
 
@@ -1070,6 +1077,9 @@ RT_DEV bool bvh_run(const DevScene& S, float delta, const f4* wrapper, const Ray
 #endif
 #ifdef RT_PROFILE_REGIONS
         ++visits;
+#endif
+#ifdef RT_PAD_BVH
+        RT_VALU_PAD(RT_PAD_BVH);
 #endif
         PROF_T0(pt);
         if (leaf_node) {
@@ -2219,8 +2229,11 @@ constexpr uint32_t kSuspLanes = RT_SUSPEND;  // suspend a BVH traversal's tail a
 // kWaves: the waves per SIMD the register allocator must allow. 3 (<= 168 VGPRs)
 // is the default; the fast kernel also exists at 4 (<= 128 VGPRs, a few spills),
 // launched when the scene's LDS stack fits four waves per SIMD (rt_render_launch).
+#ifndef RT_W4_WAVES
+#define RT_W4_WAVES 4  // A/B diagnostic: the occupancy the "4-wave" instances are compiled for
+#endif
 template <int kKind, int kWaves = 3, uint32_t kF = kFAll>
-__global__ __launch_bounds__(64, kWaves) void trace_samples(DevScene Sg, DevCamera C, DevParams P, ChunkParams Q,
+__global__ __launch_bounds__(64, kWaves == 4 ? RT_W4_WAVES : kWaves) void trace_samples(DevScene Sg, DevCamera C, DevParams P, ChunkParams Q,
                                                     float* __restrict__ sbuf, TraceCounters* __restrict__ ctr,
                                                     ReplayItem* __restrict__ replay_list, uint32_t fixup,
                                                     unsigned long long* __restrict__ seg_counter) {
@@ -2342,6 +2355,9 @@ __global__ __launch_bounds__(64, kWaves) void trace_samples(DevScene Sg, DevCame
         }
         PROF_ADD(kPrRefill, pr);
         if (__ballot(has) == 0ull) break;  // pool exhausted and every path finished
+#ifdef RT_PAD_TRIP
+        RT_VALU_PAD(RT_PAD_TRIP);
+#endif
 #ifdef RT_PROFILE_REGIONS
         if (kKind == 0) {  // throughput histogram: this iteration's segments into the current bucket
             const uint32_t b = (uint32_t)((__builtin_amdgcn_s_memrealtime() - wave_t0) / kTpTicks);
