@@ -81,6 +81,12 @@ constexpr uint32_t kModeNoStream = 1u << 17;
 // EXPERIMENT ONLY (RT_OPT_TUNE, not exact): closest-hit pruning also on BVHs the proof does not
 // cover (triangles, moving spheres), to measure what an exact bound for them could gain.
 constexpr uint32_t kModePruneAllExp = 1u << 20;
+// Block order: a shard's blocks are taken last block first (bottom image rows first), so the
+// upper rows, which in every BASELINE framing hold the background and end their paths after a
+// segment or two, are the work left when the pool runs dry and the drain is short (one rank of
+// 8: C3 69.7 -> 68.0 ms, C1 -3%). BlocksForward (RT_OPT_TUNE, A/B only) restores
+// the top-first order. Either order gives the same bits (samples are keyed by pixel and index).
+constexpr uint32_t kModeBlocksForward = 1u << 21;
 #ifdef RT_ABLATE
 // Ablation build (librtamd_ablate.so, diagnostics only): RT_OPT_TUNE bits that run a
 // piece of work twice (results of the copy discarded through an opaque test),
@@ -220,9 +226,11 @@ RT_DEV V at(const Ray& r, float t) { return r.o + t * r.d; }  // ray.rs:28-30
 // ---------------------------------------------------------------------------
 // Philox4x32-10 per-(pixel, sample) stream (replaces rand::thread_rng)
 // ---------------------------------------------------------------------------
+// d counts the draws made; draw d is word d % 4 of Philox block d / 4, whose words not
+// yet drawn wait in r0..r2 (the first is returned at once), so 6 registers stay live.
 struct Rng {
-    uint32_t sample, pixel, block, n;
-    uint32_t b0, b1, b2, b3;
+    uint32_t sample, pixel, d;
+    uint32_t r0, r1, r2;
 };
 RT_DEV void philox(uint32_t& c0, uint32_t& c1, uint32_t& c2, uint32_t& c3, uint32_t k0, uint32_t k1) {
 #pragma unroll
@@ -250,15 +258,16 @@ uint4 philox_block(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t k0, uint32_t 
     return make_uint4(c0, c1, c2, c3);
 }
 RT_DEV uint32_t next_u32(Rng& g, const Key& k) {
-    if (g.n == 0u) {
-        uint4 b = philox_block(g.block, g.sample, g.pixel, k.k0, k.k1);
-        g.b0 = b.x; g.b1 = b.y; g.b2 = b.z; g.b3 = b.w;
-        g.block += 1u;
-        g.n = 4u;
+    uint32_t r;
+    if ((g.d & 3u) == 0u) {
+        const uint4 b = philox_block(g.d >> 2, g.sample, g.pixel, k.k0, k.k1);
+        r = b.x;
+        g.r0 = b.y; g.r1 = b.z; g.r2 = b.w;
+    } else {
+        r = g.r0;
+        g.r0 = g.r1; g.r1 = g.r2;
     }
-    uint32_t r = g.b0;
-    g.b0 = g.b1; g.b1 = g.b2; g.b2 = g.b3;
-    g.n -= 1u;
+    g.d += 1u;
     return r;
 }
 RT_DEV float std01(Rng& g, const Key& k) {  // rand 0.8.5 Standard f32
@@ -1754,8 +1763,7 @@ RT_DEV void start_sample(const DevCamera& C, const DevParams& P, const Key& k, u
                          uint32_t pixel, uint32_t sample, Rng& g, Ray& ray) {
     g.sample = sample;
     g.pixel = pixel;
-    g.block = 0u;
-    g.n = 0u;
+    g.d = 0u;
     // renderer.rs:141-142
     float u = ((float)x + std01(g, k)) / (float)(P.width - 1u);
     float v = ((float)y + std01(g, k)) / (float)(P.height - 1u);
@@ -1797,6 +1805,7 @@ struct ChunkParams {
     uint32_t fast_grid;       // waves of the fast kernel's launch (the streaming replay pass waits for them)
     uint32_t nslots;          // sample-buffer plane size: 64 slots per 8x8 block of the shard, block-major
     uint32_t group;           // units per batch at most (batch_group)
+    uint32_t blocks;          // 8x8 blocks of the shard (units = blocks x samples)
 };
 
 // HittableList::hit over the world (hittable.rs:100-118), t in [0.001, inf).
@@ -2066,6 +2075,7 @@ RT_DEV bool take_sample(ItemPool& pool, bool want, const DevCamera& C, const Dev
                     blk_local += 1u;
                 }
                 if (pool.batch + (item >> 6) >= Q.units) s = Q.samples;  // past the last unit: no work
+                if (!(P.tune & kModeBlocksForward)) blk_local = Q.blocks - 1u - blk_local;
                 uint32_t pib = item & 63u;
                 sl = blk_local * 64u + pib;
                 uint32_t blk = P.shard_index + blk_local * P.shard_count;
@@ -2293,7 +2303,9 @@ __global__ __launch_bounds__(64, kWaves == 4 ? RT_W4_WAVES : kWaves) void trace_
     // A lane's pixel and chunk-local sample are its Rng's counter fields (start_sample sets
     // them), so they are not kept a second time; per-lane segment counts fit 32 bits.
     uint32_t slot = 0, take_sample_idx = 0, depth = 0;  // slot: the sample-buffer slot of the lane's pixel
-    uint32_t nseg = 0, nseg_sample = 0;
+    // A finished sample's segments are its scatters (max_depth - depth) plus, unless its last
+    // scatter took depth to 0, the segment that ended it (background or no scatter).
+    uint32_t nseg = 0;
     V L = mk(0.0f, 0.0f, 0.0f), T = mk(1.0f, 1.0f, 1.0f);
     Rng g{};
     Ray ray{};
@@ -2311,14 +2323,12 @@ __global__ __launch_bounds__(64, kWaves == 4 ? RT_W4_WAVES : kWaves) void trace_
             if (take_sample(pool, !has, C, P, Q, k, counter, list, list_n, ctr, stream_grid, sbuf, lane, slot, take_sample_idx, L, T, depth, g,
                             ray)) {
                 has = true;
-                nseg_sample = 0;
                 w.pos = 0u;
                 w.resume = false;
             }
             PROF_ADD(kPrRefill, pr);
             if (__ballot(has) == 0ull) break;  // pool exhausted and every path finished
             if (has && w.pos == 0u && !w.resume) {  // a new segment: ray.rs:43 world.hit(r, 0.001, inf)
-                nseg_sample += 1u;
                 w.closest = kInf;
                 w.any = false;
             }
@@ -2336,12 +2346,12 @@ __global__ __launch_bounds__(64, kWaves == 4 ? RT_W4_WAVES : kWaves) void trace_
                 if (shade_marble<kF>(S, P, Q, k, sbuf, walked, w.any, w.hit_entry, w.hit_code, w.closest, ray, L, T,
                                      depth, g, slot, g.sample - Q.sample0)) {
                     has = false;
-                    nseg += nseg_sample;
+                    nseg += P.max_depth - depth + (depth != 0u ? 1u : 0u);
                 }
             } else if (walked && finish_segment<kF>(S, P, Q, k, sbuf, w.any, w.hit_entry, w.hit_code, w.closest, ray, L,
                                                     T, depth, g, slot, g.sample - Q.sample0)) {
                 has = false;
-                nseg += nseg_sample;
+                nseg += P.max_depth - depth + (depth != 0u ? 1u : 0u);
             }
             if (walked) w.pos = 0u;
         }
@@ -2351,7 +2361,6 @@ __global__ __launch_bounds__(64, kWaves == 4 ? RT_W4_WAVES : kWaves) void trace_
         if (take_sample(pool, !has, C, P, Q, k, counter, list, list_n, ctr, stream_grid, sbuf, lane, slot, take_sample_idx, L, T, depth, g,
                         ray)) {
             has = true;
-            nseg_sample = 0;
         }
         PROF_ADD(kPrRefill, pr);
         if (__ballot(has) == 0ull) break;  // pool exhausted and every path finished
@@ -2374,7 +2383,6 @@ __global__ __launch_bounds__(64, kWaves == 4 ? RT_W4_WAVES : kWaves) void trace_
             float t = 0.0f;
             uint32_t he = 0, hc = 0;
             if (has) {
-                nseg_sample += 1u;
                 bool replay = false;
                 PROF_T0(pw);
                 any = world_hit<kKind, kF>(S, P.prune_delta, ray, g, k, t, he, hc, stk, mode, replay);
@@ -2389,10 +2397,9 @@ __global__ __launch_bounds__(64, kWaves == 4 ? RT_W4_WAVES : kWaves) void trace_
             }
             if (shade_marble<kF>(S, P, Q, k, sbuf, shade, any, he, hc, t, ray, L, T, depth, g, slot, g.sample - Q.sample0)) {
                 has = false;
-                nseg += nseg_sample;
+                nseg += P.max_depth - depth + (depth != 0u ? 1u : 0u);
             }
         } else if (has) {
-            nseg_sample += 1u;
             float t;
             uint32_t he = 0, hc = 0;
             bool replay = false;
@@ -2405,7 +2412,7 @@ __global__ __launch_bounds__(64, kWaves == 4 ? RT_W4_WAVES : kWaves) void trace_
                 has = false;
             } else if (finish_segment<kF>(S, P, Q, k, sbuf, any, he, hc, t, ray, L, T, depth, g, slot, g.sample - Q.sample0)) {
                 has = false;
-                nseg += nseg_sample;
+                nseg += P.max_depth - depth + (depth != 0u ? 1u : 0u);
             }
         }
     }
@@ -3201,6 +3208,7 @@ int rt_render_launch_camera(rt_scene_handle s, const rt_camera* camera, const rt
         q.sample0 = p->sample_base + c * chunk;
         q.samples = c + 1 < nchunks ? chunk : p->samples_per_pixel - c * chunk;
         q.units = (uint32_t)(nblk * (uint64_t)q.samples);
+        q.blocks = (uint32_t)nblk;
         q.group = batch_group(q.units, exact || dev_ref.hrpp_tab ? (uint32_t)s->grid_ref : (uint32_t)s->grid);
         if (const int64_t gr = opt(RT_OPT_GROUP)) q.group = (uint32_t)gr;  // diagnostics / A-B runs
         if (q.group > q.samples) q.group = q.samples;  // a batch crosses at most one block boundary

@@ -225,6 +225,31 @@ def test_gpu_shards_compose_bit_identically(n, rt):
     np.testing.assert_array_equal(acc, full)
 
 
+@pytest.mark.parametrize("n", [1, 3])
+def test_block_order_does_not_change_the_image(n, rt, orc):
+    # The fast kernel takes a shard's blocks last first (bottom rows first: a short drain);
+    # RT_OPT_TUNE bit 21 restores the top-first order. Samples are keyed by pixel and global
+    # index and resolved per slot in sample order, so both orders give the oracle's bits, for
+    # the whole frame and for a shard (a ragged 61 x 35 image: partial blocks at both edges).
+    cfg, scene, params = setup(rt, "C3", 61, 3)
+    want, cnt = orc.render(scene, cfg.camera(), params)
+    for tune in (0, 1 << 21):
+        with rt.options(tune=tune):
+            ds = rt.DeviceScene(scene)
+            try:
+                acc = np.zeros_like(want)
+                segs = 0
+                for k in range(n):
+                    p = rt.render_params(cfg.width, cfg.height, cfg.spp, cfg.depth, background=cfg.background(),
+                                         seed=1, shard_index=k, shard_count=n)
+                    _, st = ds.render(cfg.camera(), p, out=acc)
+                    segs += st["segments"]
+            finally:
+                ds.close()
+        np.testing.assert_array_equal(acc, want)
+        assert segs == cnt["segments"]
+
+
 def test_repeat_renders_are_bit_identical(rt):
     cfg, scene, params = setup(rt, "C5", 64, 4)
     ds = rt.DeviceScene(scene)
