@@ -216,6 +216,13 @@ RT_DEV f4 ld4(const f4* p) {
     float4 v = *reinterpret_cast<const float4*>(p);
     return f4{v.x, v.y, v.z, v.w};
 }
+// Row loads at a 32-bit byte offset from a wave-uniform base (BVH4 nodes).
+RT_DEV f4 ld4_at(const f4* base, uint32_t byte_off) {
+    return ld4(reinterpret_cast<const f4*>(reinterpret_cast<const char*>(base) + byte_off));
+}
+RT_DEV float2 ld2_at(const f4* base, uint32_t byte_off) {
+    return *reinterpret_cast<const float2*>(reinterpret_cast<const char*>(base) + byte_off);
+}
 
 struct Ray {
     V o, d;
@@ -582,7 +589,7 @@ RT_DEV bool slab(float x0, float y0, float z0, float x1, float y1, float z1, con
 // candidate inside it would then compute t > closest (exact pruning).
 RT_DEV float prune_bound(float closest) { return closest + __builtin_fabsf(closest) * 0x1p-19f; }
 
-// Conservative leaf test (prunable BVHs only, leaf_intervals2 +
+// Conservative leaf test (prunable BVHs only, leaf_intervals2_nf +
 // leaf_interval_may_hit): false only when the leaf's primitive provably has no hit
 // in [tmin, closest]. The box is the primitive's own bounding box inflated by
 // delta; any computed hit t lies on the ray within rounding distance (<< delta) of
@@ -854,7 +861,10 @@ RT_DEV bool bvh_hit_hrpp(const DevScene& S, uint32_t wrapper2, uint32_t pid, con
 }
 // child_key for all four slots of a node at once, on two children per packed
 // f32 instruction (v_pk_add_f32 / v_pk_mul_f32: the same correctly rounded IEEE
-// operations per element). Valid only without NaN slab values: the fast kernel
+// operations per element). The rows come ordered by the ray's direction signs (bvh_run
+// loads them so): n* hold each axis's near plane (the max plane when 1/d < 0, aabb.rs:33-35's
+// swap), f* the far one, so each slab value is the reference's (plane - o) * inv and no
+// per-child select is left. Valid only without NaN slab values: the fast kernel
 // replays every ray with a zero or non-finite 1/d component, so (plane - o) * inv
 // is finite or +-inf, never 0 * inf, and the reference's sequential
 // `if a > t_min {a} else {t_min}` clamps (aabb.rs:28-41) equal max/min. Empty
@@ -862,52 +872,47 @@ RT_DEV bool bvh_hit_hrpp(const DevScene& S, uint32_t wrapper2, uint32_t pid, con
 // pb = +inf when the BVH is not prunable.
 typedef float pk2 __attribute__((ext_vector_type(2)));
 RT_DEV pk2 pk(float a, float b) { return pk2{a, b}; }
-RT_DEV void child_keys4(f4 mnx, f4 mny, f4 mnz, f4 mxx, f4 mxy, f4 mxz, const Ray& r, V inv, float tmin,
-                        float tmax_entry, float pb, float dmi, float key[4]) {
+RT_DEV void child_keys4_nf(f4 nx, f4 ny, f4 nz, f4 fx, f4 fy, f4 fz, const Ray& r, V inv, float tmin,
+                           float tmax_entry, float pb, float dmi, float key[4]) {
     const pk2 ox = pk(r.o.x, r.o.x), oy = pk(r.o.y, r.o.y), oz = pk(r.o.z, r.o.z);
     const pk2 ix = pk(inv.x, inv.x), iy = pk(inv.y, inv.y), iz = pk(inv.z, inv.z);
-    const bool sx = inv.x < 0.0f, sy = inv.y < 0.0f, sz = inv.z < 0.0f;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-        const pk2 ax = (h ? pk(mnx.z, mnx.w) : pk(mnx.x, mnx.y)) - ox, bx = (h ? pk(mxx.z, mxx.w) : pk(mxx.x, mxx.y)) - ox;
-        const pk2 ay = (h ? pk(mny.z, mny.w) : pk(mny.x, mny.y)) - oy, by = (h ? pk(mxy.z, mxy.w) : pk(mxy.x, mxy.y)) - oy;
-        const pk2 az = (h ? pk(mnz.z, mnz.w) : pk(mnz.x, mnz.y)) - oz, bz = (h ? pk(mxz.z, mxz.w) : pk(mxz.x, mxz.y)) - oz;
-        const pk2 tax = ax * ix, tbx = bx * ix, tay = ay * iy, tby = by * iy, taz = az * iz, tbz = bz * iz;
+        const pk2 tnx = ((h ? pk(nx.z, nx.w) : pk(nx.x, nx.y)) - ox) * ix, tfx = ((h ? pk(fx.z, fx.w) : pk(fx.x, fx.y)) - ox) * ix;
+        const pk2 tny = ((h ? pk(ny.z, ny.w) : pk(ny.x, ny.y)) - oy) * iy, tfy = ((h ? pk(fy.z, fy.w) : pk(fy.x, fy.y)) - oy) * iy;
+        const pk2 tnz = ((h ? pk(nz.z, nz.w) : pk(nz.x, nz.y)) - oz) * iz, tfz = ((h ? pk(fz.z, fz.w) : pk(fz.x, fz.y)) - oz) * iz;
 #pragma unroll
         for (int e = 0; e < 2; ++e) {
-            const float nx = sx ? tbx[e] : tax[e], fx = sx ? tax[e] : tbx[e];
-            const float ny = sy ? tby[e] : tay[e], fy = sy ? tay[e] : tby[e];
-            const float nz = sz ? tbz[e] : taz[e], fz = sz ? taz[e] : tbz[e];
-            const float lo = __builtin_fmaxf(__builtin_fmaxf(nx, ny), __builtin_fmaxf(nz, tmin));
-            const float hi = __builtin_fminf(__builtin_fminf(fx, fy), __builtin_fminf(fz, tmax_entry));
+            const float lo = __builtin_fmaxf(__builtin_fmaxf(tnx[e], tny[e]), __builtin_fmaxf(tnz[e], tmin));
+            const float hi = __builtin_fminf(__builtin_fminf(tfx[e], tfy[e]), __builtin_fminf(tfz[e], tmax_entry));
             const float te = lo - dmi;
             const bool go = lo <= hi && te <= pb;  // = !(hi < lo) && !(te > pb) without NaN
             key[2 * h + e] = go ? __builtin_fminf(te, 3.4028235e38f) : kInf;
         }
     }
 }
-// The two leaf slots of a leaf node: the slab interval of each leaf's box
-// inflated by delta, both leaves per packed
-// instruction. The inflation is folded into shifted origins: x0 - (o + delta)
-// carries the same error structure as (x0 - delta) - o (one rounding of a
-// coordinate-sized value, <= 2^-24 R << delta, then relative roundings). NaN-free
-// under the same 1/d condition as child_keys4; an empty second slot (inverted
-// infinite box) gives lo = +inf.
-RT_DEV void leaf_intervals2(float2 bx0, float2 by0, float2 bz0, float2 bx1, float2 by1, float2 bz1, const Ray& r,
-                            V inv, float delta, float lo[2], float hi[2]) {
-    const pk2 px = pk(r.o.x + delta, r.o.x + delta), py = pk(r.o.y + delta, r.o.y + delta),
-              pz = pk(r.o.z + delta, r.o.z + delta);
-    const pk2 mx = pk(r.o.x - delta, r.o.x - delta), my = pk(r.o.y - delta, r.o.y - delta),
-              mz = pk(r.o.z - delta, r.o.z - delta);
-    const pk2 ix = pk(inv.x, inv.x), iy = pk(inv.y, inv.y), iz = pk(inv.z, inv.z);
-    const pk2 tax = (pk(bx0.x, bx0.y) - px) * ix, tbx = (pk(bx1.x, bx1.y) - mx) * ix;
-    const pk2 tay = (pk(by0.x, by0.y) - py) * iy, tby = (pk(by1.x, by1.y) - my) * iy;
-    const pk2 taz = (pk(bz0.x, bz0.y) - pz) * iz, tbz = (pk(bz1.x, bz1.y) - mz) * iz;
+// The two leaf slots of a leaf node: the slab interval of each leaf's box inflated by
+// delta, both leaves per packed instruction, on sign-ordered rows like child_keys4_nf. The
+// inflation is folded into shifted origins: x0 - (o + delta) for a min plane, x1 - (o - delta)
+// for a max one, with the error structure of (x0 - delta) - o (one rounding of a
+// coordinate-sized value, <= 2^-24 R << delta, then relative roundings). NaN-free under the
+// same 1/d condition as child_keys4_nf; an empty second slot (inverted infinite box) gives
+// lo = +inf.
+RT_DEV void leaf_intervals2_nf(float2 nx, float2 ny, float2 nz, float2 fx, float2 fy, float2 fz, const Ray& r,
+                               V inv, float delta, float lo[2], float hi[2]) {
     const bool sx = inv.x < 0.0f, sy = inv.y < 0.0f, sz = inv.z < 0.0f;
+    const float pxs = r.o.x + delta, pys = r.o.y + delta, pzs = r.o.z + delta;
+    const float mxs = r.o.x - delta, mys = r.o.y - delta, mzs = r.o.z - delta;
+    const float anx = sx ? mxs : pxs, afx = sx ? pxs : mxs, sny = sy ? mys : pys, afy = sy ? pys : mys;
+    const float anz = sz ? mzs : pzs, afz = sz ? pzs : mzs;
+    const pk2 ix = pk(inv.x, inv.x), iy = pk(inv.y, inv.y), iz = pk(inv.z, inv.z);
+    const pk2 tnx = (pk(nx.x, nx.y) - pk(anx, anx)) * ix, tfx = (pk(fx.x, fx.y) - pk(afx, afx)) * ix;
+    const pk2 tny = (pk(ny.x, ny.y) - pk(sny, sny)) * iy, tfy = (pk(fy.x, fy.y) - pk(afy, afy)) * iy;
+    const pk2 tnz = (pk(nz.x, nz.y) - pk(anz, anz)) * iz, tfz = (pk(fz.x, fz.y) - pk(afz, afz)) * iz;
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
-        lo[e] = __builtin_fmaxf(__builtin_fmaxf(sx ? tbx[e] : tax[e], sy ? tby[e] : tay[e]), sz ? tbz[e] : taz[e]);
-        hi[e] = __builtin_fminf(__builtin_fminf(sx ? tax[e] : tbx[e], sy ? tay[e] : tby[e]), sz ? taz[e] : tbz[e]);
+        lo[e] = __builtin_fmaxf(__builtin_fmaxf(tnx[e], tny[e]), tnz[e]);
+        hi[e] = __builtin_fminf(__builtin_fminf(tfx[e], tfy[e]), tfz[e]);
     }
 }
 // The conservative leaf test's decision on a precomputed inflated interval.
@@ -1037,6 +1042,9 @@ RT_DEV bool bvh_run(const DevScene& S, float delta, const f4* wrapper, const Ray
     const bool prune = (__float_as_uint(wrapper[7].w) & rtdev::kBvhPrunable) != 0u || (mode & kModePruneAllExp);
     const float dmi = delta * fmaxf(fmaxf(__builtin_fabsf(inv.x), __builtin_fabsf(inv.y)), __builtin_fabsf(inv.z));
     const bool leaf_boxes = prune && !(mode & kModeNoLeafBoxes);
+    // Byte offsets of each axis's near-plane row in a node (min.a rows 0-2, max.a rows 3-5;
+    // the max plane is entered first when 1/d < 0); the far row is the other one (off ^ c).
+    const uint32_t onx = inv.x < 0.0f ? 48u : 0u, ony = inv.y < 0.0f ? 64u : 16u, onz = inv.z < 0.0f ? 80u : 32u;
     bool any = tv.any;
     uint32_t best_rank = tv.best_rank, sp = tv.sp, cur = tv.cur;
     bool finished = true;
@@ -1073,10 +1081,10 @@ RT_DEV bool bvh_run(const DevScene& S, float delta, const f4* wrapper, const Ray
             }
         }
         const bool leaf_node = (cur & rtdev::kLeafNodeFlag) != 0u;
-        const f4* nd = S.nodes + (size_t)(cur & ~(rtdev::kLeafNodeFlag | kDeferBit)) * rtdev::kBvhNodeF4;
+        const uint32_t nbo = (cur & ~(rtdev::kLeafNodeFlag | kDeferBit)) * (rtdev::kBvhNodeF4 * 16u);
 #else
         const bool leaf_node = (cur & rtdev::kLeafNodeFlag) != 0u;
-        const f4* nd = S.nodes + (size_t)(cur & ~rtdev::kLeafNodeFlag) * rtdev::kBvhNodeF4;
+        const uint32_t nbo = (cur & ~rtdev::kLeafNodeFlag) * (rtdev::kBvhNodeF4 * 16u);  // node byte offset
 #endif
 #ifdef RT_LEAF_AUDIT
         if ((cur & ~(rtdev::kLeafNodeFlag | kDeferBit)) >= S.num_nodes || sp > S.stack_depth + S.spill_depth) {
@@ -1101,18 +1109,25 @@ RT_DEV bool bvh_run(const DevScene& S, float delta, const f4* wrapper, const Ray
             // rounded t equals another candidate's passes or fails depending on
             // which t_max it saw. The node result then joins (closest, DFS rank)
             // like the tree-min does.
-            const float2 bx0 = ld2(nd, 0), by0 = ld2(nd, 1), bz0 = ld2(nd, 2), bx1 = ld2(nd, 3), by1 = ld2(nd, 4),
-                         bz1 = ld2(nd, 5), chs = ld2(nd, 6), rks = ld2(nd, 7);
+            const f4* nd = S.nodes;
+            const float2 nx2 = ld2_at(nd, nbo + onx), ny2 = ld2_at(nd, nbo + ony), nz2 = ld2_at(nd, nbo + onz),
+                         fx2 = ld2_at(nd, nbo + (onx ^ 48u)), fy2 = ld2_at(nd, nbo + (ony ^ 80u)),
+                         fz2 = ld2_at(nd, nbo + (onz ^ 112u)), chs = ld2_at(nd, nbo + 96u), rks = ld2_at(nd, nbo + 112u);
             float tmr = tmax_entry, nt = 0.0f;
             bool nh = false;
             uint32_t ncode = 0u, nrank = 0u;
             const uint32_t nleaf = __float_as_uint(chs.y) == rtdev::kChildEmpty ? 1u : 2u;
             float llo[2] = {-kInf, -kInf}, lhi[2] = {kInf, kInf};
-            if (leaf_boxes) leaf_intervals2(bx0, by0, bz0, bx1, by1, bz1, r, inv, delta, llo, lhi);
+            if (leaf_boxes) leaf_intervals2_nf(nx2, ny2, nz2, fx2, fy2, fz2, r, inv, delta, llo, lhi);
             for (uint32_t k = 0; k < nleaf; ++k) {
                 const uint32_t lcode = __float_as_uint(k ? chs.y : chs.x), rank = __float_as_uint(k ? rks.y : rks.x);
-                [[maybe_unused]] const float x0 = k ? bx0.y : bx0.x, y0 = k ? by0.y : by0.x, z0 = k ? bz0.y : bz0.x;
-                [[maybe_unused]] const float x1 = k ? bx1.y : bx1.x, y1 = k ? by1.y : by1.x, z1 = k ? bz1.y : bz1.x;
+#ifdef RT_LEAF_AUDIT
+                const float2 bx0 = ld2(S.nodes + nbo / 16u, 0), by0 = ld2(S.nodes + nbo / 16u, 1),
+                             bz0 = ld2(S.nodes + nbo / 16u, 2), bx1 = ld2(S.nodes + nbo / 16u, 3),
+                             by1 = ld2(S.nodes + nbo / 16u, 4), bz1 = ld2(S.nodes + nbo / 16u, 5);
+                const float x0 = k ? bx0.y : bx0.x, y0 = k ? by0.y : by0.x, z0 = k ? bz0.y : bz0.x;
+                const float x1 = k ? bx1.y : bx1.x, y1 = k ? by1.y : by1.x, z1 = k ? bz1.y : bz1.x;
+#endif
                 // the right leaf can only matter if t <= min(closest, left t)
                 const float bound = tmr < closest ? tmr : closest;
                 if (!leaf_boxes || leaf_interval_may_hit(k ? llo[1] : llo[0], k ? lhi[1] : lhi[0], tmin, bound)) {
@@ -1156,13 +1171,18 @@ RT_DEV bool bvh_run(const DevScene& S, float delta, const f4* wrapper, const Ray
         uint32_t c0 = rtdev::kChildEmpty, c1 = rtdev::kChildEmpty, c2 = rtdev::kChildEmpty, c3 = rtdev::kChildEmpty;
         if (!leaf_node) {
             // interior slots: reference box test, prune bound, nearest first
-            const f4 mnx = ld4(nd), mny = ld4(nd + 1), mnz = ld4(nd + 2), mxx = ld4(nd + 3), mxy = ld4(nd + 4),
-                     mxz = ld4(nd + 5), chf = ld4(nd + 6);
+            const f4* nd = S.nodes;
+            const f4 nx = ld4_at(nd, nbo + onx), ny = ld4_at(nd, nbo + ony), nz = ld4_at(nd, nbo + onz),
+                     fx = ld4_at(nd, nbo + (onx ^ 48u)), fy = ld4_at(nd, nbo + (ony ^ 80u)),
+                     fz = ld4_at(nd, nbo + (onz ^ 112u)), chf = ld4_at(nd, nbo + 96u);
             c0 = __float_as_uint(chf.x);
             c1 = __float_as_uint(chf.y);
             c2 = __float_as_uint(chf.z);
             c3 = __float_as_uint(chf.w);
-            ABLATE(kAbKeys2, float k2 = child_key(mnx.x, mny.x, mnz.x, mxx.x, mxy.x, mxz.x, r, inv, tmin, tmax_entry,
+            ABLATE(kAbKeys2, const f4 mnx = inv.x < 0.0f ? fx : nx; const f4 mxx = inv.x < 0.0f ? nx : fx;
+                   const f4 mny = inv.y < 0.0f ? fy : ny; const f4 mxy = inv.y < 0.0f ? ny : fy;
+                   const f4 mnz = inv.z < 0.0f ? fz : nz; const f4 mxz = inv.z < 0.0f ? nz : fz;
+                   float k2 = child_key(mnx.x, mny.x, mnz.x, mxx.x, mxy.x, mxz.x, r, inv, tmin, tmax_entry,
                                                   closest, prune, dmi) +
                                         child_key(mnx.y, mny.y, mnz.y, mxx.y, mxy.y, mxz.y, r, inv, tmin, tmax_entry,
                                                   closest, prune, dmi) +
@@ -1172,8 +1192,8 @@ RT_DEV bool bvh_run(const DevScene& S, float delta, const f4* wrapper, const Ray
                                                   closest, prune, dmi);
                    if (k2 == -1.0f) c0 = 0u;);
             float key[4];
-            child_keys4(mnx, mny, mnz, mxx, mxy, mxz, r, inv, tmin, tmax_entry, prune ? prune_bound(closest) : kInf,
-                        prune ? dmi : 0.0f, key);
+            child_keys4_nf(nx, ny, nz, fx, fy, fz, r, inv, tmin, tmax_entry, prune ? prune_bound(closest) : kInf,
+                           prune ? dmi : 0.0f, key);
             t0 = key[0];
             t1 = key[1];
             t2 = key[2];
@@ -2511,8 +2531,10 @@ __global__ void kat_eval(int op, const float* __restrict__ in, float* __restrict
             const float E = kInf;
             f4 mnx{a[0], E, E, E}, mny{a[1], E, E, E}, mnz{a[2], E, E, E};
             f4 mxx{a[3], -E, -E, -E}, mxy{a[4], -E, -E, -E}, mxz{a[5], -E, -E, -E};
-            float key[4];
-            child_keys4(mnx, mny, mnz, mxx, mxy, mxz, r, inv, a[12], a[13], kInf, 0.0f, key);
+            float key[4];  // rows ordered by the direction signs, as bvh_run loads them
+            child_keys4_nf(inv.x < 0.0f ? mxx : mnx, inv.y < 0.0f ? mxy : mny, inv.z < 0.0f ? mxz : mnz,
+                           inv.x < 0.0f ? mnx : mxx, inv.y < 0.0f ? mny : mxy, inv.z < 0.0f ? mnz : mxz, r, inv,
+                           a[12], a[13], kInf, 0.0f, key);
             r0 = key[0] != kInf ? 1.0f : 0.0f;
             r1 = key[0];
         }
