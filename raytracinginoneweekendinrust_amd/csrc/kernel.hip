@@ -3175,7 +3175,13 @@ int rt_render_launch_camera(rt_scene_handle s, const rt_camera* camera, const rt
             return hip_fail(e, "hipEventCreate (replay stream)");
     }
     // The fast kernel's instance: four waves per SIMD when that raises its occupancy
-    // over three (the Perlin tables then stay in L2, so the stack alone sets LDS).
+    // over three (the Perlin tables then stay in L2, so the stack alone sets LDS) — except
+    // for the BVH-only and triangle-BVH presets, whose 4-wave instances spill more than the
+    // extra wave buys (same box, 3 vs 4 waves: C1 4.1 vs 4.4 ms, C4 at 50 spp 112.1 vs
+    // 121.4 ms; the Marble, sphere-run and flat presets stay at 4: C3 +14%, C2 +12%, C5 +10%
+    // at 3; profiles/r02/w3/).
+    const uint32_t preset_feats = s->features & ~kFDeep;
+    const bool prefer3 = preset_feats == kFBvh || preset_feats == (kFBvh | kFTri);
     if (s->fast_waves == 0) {
         const size_t stack_lds = (size_t)s->dev.stack_depth * 128u * sizeof(uint32_t);
         const size_t perm3 = s->dev.perm_bytes != 0u && s->dev.perm_bytes <= kPermLdsMax ? s->dev.perm_bytes : 0u;
@@ -3183,7 +3189,7 @@ int rt_render_launch_camera(rt_scene_handle s, const rt_camera* camera, const rt
         const TraceKernel k3 = fast_instance(3, s->features), k4 = fast_instance(4, s->features);
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per3, k3, 64, stack_lds + perm3) != hipSuccess) per3 = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per4, k4, 64, stack_lds) != hipSuccess) per4 = 0;
-        s->fast_waves = per4 > per3 && !(dp.tune & kModeW3) ? 4 : 3;
+        s->fast_waves = per4 > per3 && !(dp.tune & kModeW3) && !prefer3 ? 4 : 3;
     }
     if (s->fast_waves == 4) dp.tune |= kModeNoPermLds;
     // LDS per wave: the kernel's traversal stack, then the Perlin tables
