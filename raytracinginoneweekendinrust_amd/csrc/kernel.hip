@@ -2272,7 +2272,7 @@ RT_DEV bool shade_marble(const DevScene& S, const DevParams& P, const ChunkParam
 // fixup kernel re-renders the whole chunk and takes back the fast kernel's
 // segment count.
 #ifndef RT_SUSPEND
-#define RT_SUSPEND 16
+#define RT_SUSPEND 24  // C4 at 3 waves, 50 spp: 8 129 ms, 16 112.4, 20 109.1, 24 108.0, 28 108.7, 32 111.1
 #endif
 constexpr uint32_t kSuspLanes = RT_SUSPEND;  // suspend a BVH traversal's tail at this many lanes or fewer
 // kWaves: the waves per SIMD the register allocator must allow. 3 (<= 168 VGPRs)
