@@ -22,7 +22,6 @@ from __future__ import annotations
 import argparse
 import json
 import os
-import subprocess
 import sys
 import time
 
@@ -53,15 +52,13 @@ def bytes_per_sample(counters: dict, spp: int) -> float:
 
 
 def host_nproc() -> int:
-    """`nproc`: the CPUs this process may run on (its affinity / cgroup share)."""
-    try:
-        return int(subprocess.run(["nproc"], capture_output=True, text=True, check=True).stdout.strip())
-    except Exception:
-        return len(os.sched_getaffinity(0))
+    """The CPUs this process may run on (its affinity mask: what `nproc` prints, without
+    starting a program from a GPU-initialised process)."""
+    return len(os.sched_getaffinity(0))
 
 
 def cpu_threads() -> int:
-    """Threads for the CPU baseline: every CPU `nproc` reports, capped by OMP_NUM_THREADS where the
+    """Threads for the CPU baseline: every CPU of the affinity mask, capped by OMP_NUM_THREADS where the
     launcher sets the box's CPU share (16 per GPU on the GPU pool, whose nproc shows the whole host)."""
     n = host_nproc()
     env = os.environ.get("OMP_NUM_THREADS")
@@ -70,17 +67,31 @@ def cpu_threads() -> int:
     return max(1, n)
 
 
-VALU_PMC = os.path.join(ROOT, "profiles", "pmc_valu.json")
+PMC_DIRS = (os.path.join(ROOT, "profiles", "r03"), os.path.join(ROOT, "profiles"))
 
 
-def valu_roofline(cfg_name: str):
-    """The trace kernel's real roofline (vector-ALU issue), from the committed PMC summary
-    tools/valu_roofline.py writes (issue fraction, lane utilisation, instructions per segment)."""
-    try:
-        j = json.load(open(VALU_PMC))
-    except Exception:
-        return None
-    return j if j.get("config") == cfg_name else None
+def library_md5() -> str:
+    """md5 of the librtamd.so this process loaded (the PMC summaries record the one they profiled)."""
+    import hashlib
+
+    from raytracinginoneweekendinrust_amd import _capi
+    with open(_capi.LIB_PATH, "rb") as f:
+        return hashlib.md5(f.read()).hexdigest()
+
+
+def pmc_summary(kind: str, cfg_name: str, md5: str):
+    """A committed PMC summary (tools/valu_roofline.py: kind 'valu' or 'traffic') of `cfg_name`'s
+    trace kernel, or None. Only a summary that records the md5 of the very library this process
+    loaded counts: after any rebuild without a re-profile the line carries null, not stale counters."""
+    for d in PMC_DIRS:
+        for name in (f"pmc_{kind}_{cfg_name}.json", f"pmc_{kind}.json"):
+            try:
+                j = json.load(open(os.path.join(d, name)))
+            except Exception:
+                continue
+            if j.get("config") == cfg_name and j.get("library_md5") == md5:
+                return j
+    return None
 
 
 SUBSAMPLE = 64  # SURVEY.md §8(d): counts from a fixed 1/64 subsample at the config's spp and depth
@@ -127,6 +138,8 @@ def main() -> int:
     ap.add_argument("--scaling", choices=["weak", "strong"], default="strong")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--exact-bvh", action="store_true")
+    ap.add_argument("--gather", choices=["auto", "ipc", "shm"], default="auto",
+                    help="N>1 frame gather transport (frame_gather.FrameGather)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -164,7 +177,7 @@ def main() -> int:
     gather = None
     if args.scaling == "strong" and world > 1:
         from raytracinginoneweekendinrust_amd.frame_gather import FrameGather
-        gather = FrameGather(W, H, rank, world, device=f"cuda:{local_rank}")
+        gather = FrameGather(W, H, rank, world, device=f"cuda:{local_rank}", transport=args.gather)
     frame = [out]
 
     def step():
@@ -217,9 +230,10 @@ def main() -> int:
             cnt = oracle_measure(cfg, scene, threads)
             if world == 1 and not args.no_cpu_baseline:
                 cpu = {"value": cnt["samples"] / cnt["seconds"] / 1e6, "unit": "Msamples/s", "cores": cnt["threads"],
-                       "kind": "port", "host_nproc": host_nproc(),
+                       "kind": "port", "label": "oracle restatement (C, pthreads)", "host_nproc": host_nproc(),
                        "note": "the C oracle restatement of the reference (oracle/oracle.c), the Rust reference "
-                               "cannot be built here; threads = nproc capped by OMP_NUM_THREADS (the box's CPU share)",
+                               "cannot be built here; threads = the affinity mask capped by OMP_NUM_THREADS "
+                               "(the box's CPU share)",
                        "sample": f"{cfg.name} 8x8 blocks b % {SUBSAMPLE} == 21 ({cnt['samples'] // spp} px, 1/64 of "
                                  f"the frame) at {spp} spp depth {cfg.depth}: {cnt['samples']} samples in "
                                  f"{cnt['seconds']:.1f}s (C oracle, pthreads)"}
@@ -229,16 +243,12 @@ def main() -> int:
         b_sample = bytes_per_sample(cnt, spp) if cnt else None
         samples_per_trace_launch = samples_rank_launch * args.steps / max(trace_launches, 1)
         achieved = (b_sample * samples_per_trace_launch / (kernel_ms / 1e3) / 1e9) if b_sample else None
-        traffic = None
-        pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-        if os.path.exists(pmc) and world == 1:
-            try:
-                j = json.load(open(pmc))
-                if j.get("config") == cfg.name:
-                    traffic = j.get("hbm_bytes_per_launch")
-            except Exception:
-                traffic = None
-        valu = valu_roofline(cfg.name) if world == 1 else None
+        md5 = library_md5()
+        tj = pmc_summary("traffic", cfg.name, md5) if world == 1 else None
+        traffic = tj.get("hbm_bytes_per_launch") if tj else None
+        valu = pmc_summary("valu", cfg.name, md5) if world == 1 else None
+        if valu:
+            valu = {k: v for k, v in valu.items() if k != "counters"}
         value = total_samples / wall_max / 1e6
         line = {
             # BASELINE.json's metric is quoted on C3; the other configs name their own workload
@@ -259,22 +269,26 @@ def main() -> int:
                        "scene": cfg.scene, "width": W, "height": H, "spp": spp, "max_depth": cfg.depth,
                        "parallelism": ("weak: full frame per GPU, disjoint sample ranges" if args.scaling == "weak"
                                        else f"strong: one fixed frame, 8x8 blocks b % {world} == rank per GPU, shards "
-                                            "gathered to rank 0 inside the timed region (shared-memory hipMemcpyAsync "
-                                            "D2H + H2D + rt_shard_unpack; no collective)" if world > 1
+                                            "gathered to rank 0 inside the timed region (rt_shard_pack, then "
+                                            "hipMemcpyAsync into rank 0's IPC-mapped buffer, or the /dev/shm bounce; "
+                                            "rt_shard_unpack; no collective)" if world > 1
                                        else "one GPU: the whole frame"),
+                       "gather": gather.transport if gather is not None else None,
                        "exact_bvh": args.exact_bvh},
             "rays_per_s": seg_total / wall_max,
             "segments_per_sample": seg_total / total_samples if total_samples else None,
             "image_finite": img_ok,
             "frame_sum": frame_sum,
-            "roofline": {"bound": "valu", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
                          "achieved_is": "SURVEY.md §8(d) algorithmic bytes per sample (the reference algorithm's "
                                         "scene reads, counted by the oracle) x samples / trace-kernel time: an "
                                         "L2 scene-read rate (the scene is L2-resident), priced against HBM peak "
-                                        "as §8(d) asks; the kernel's actual limit is vector-ALU issue (valu)",
+                                        "as §8(d) asks; the kernel's measured limit is in `valu` (vector-ALU "
+                                        "lane throughput against the measured issue peak), not HBM",
                          "traffic_GBs": (traffic / (kernel_ms / 1e3) / 1e9) if traffic else None,
                          "valu": valu,
+                         "pmc_library_md5": md5,
                          "kernel": "trace_samples", "kernel_ms": kernel_ms, "launches_per_step":
                              trace_launches / args.steps, "step_device_ms": step_ms,
                          "bytes_per_sample": b_sample, "samples_per_launch": samples_per_trace_launch},

@@ -82,8 +82,9 @@ typedef enum rt_node_kind {
     RT_OBJ_BVH_TREE = 44      /* an already built Bvh (bvh.rs:38-43): its BvhNode array
                                  as the reference holds it. ref[0] first rt_bvh_node of
                                  the tree in rt_scene_desc.bvh_nodes, ref[1] node count,
-                                 ref[2] root_index (relative to ref[0]), f[0] time0,
-                                 f[1] time1 (unused by the hot path), f[2] = 1: built
+                                 ref[2] root_index (relative to ref[0]), f[0] / f[1]
+                                 ignored (the reference's Bvh stores no shutter times),
+                                 f[2] = 1: built
                                  with Bvh::with_predictor (HRPP only). The device
                                  traverses this tree as given: its shape and boxes
                                  decide every box test and every DFS-rank tie. */
@@ -343,6 +344,20 @@ int rt_shard_pack(const float* d_image, uint32_t width, uint32_t height, uint32_
                   uint32_t n, float* d_packed, void* stream);
 int rt_shard_unpack(const float* d_packed_all, uint32_t width, uint32_t height,
                     uint32_t n, float* d_image, void* stream);
+
+/* Peer transport for that gather (the north-star's hipMemcpyAsync gather to rank 0,
+ * device to device over xGMI): rank 0 exports its gather buffer (rt_ipc_export: the
+ * hipIpcMemHandle_t of the allocation holding d_ptr plus d_ptr's offset in it, in
+ * RT_IPC_HANDLE_BYTES bytes the caller sends to the other ranks), every other rank
+ * maps it once (rt_ipc_open, on its own device; unmap with rt_ipc_close) and copies its
+ * packed shard into its slot with rt_copy_async (a device-to-device hipMemcpyAsync on
+ * `stream`). Replaces renderer.rs:86-95's host-side composite of the tiles; a /dev/shm
+ * bounce stays the caller's fallback where IPC is refused. */
+#define RT_IPC_HANDLE_BYTES 72
+int rt_ipc_export(const void* d_ptr, int device, uint8_t handle[RT_IPC_HANDLE_BYTES]);
+int rt_ipc_open(const uint8_t handle[RT_IPC_HANDLE_BYTES], int device, void** d_ptr);
+int rt_ipc_close(void* d_ptr, int device);
+int rt_copy_async(void* d_dst, const void* d_src, uint64_t bytes, void* stream);
 
 /* Scene builders restated from src/main.rs:185-829 ("random-spheres",
  * "random-moving-spheres", "two-spheres", "marble", "earth", "simple-lights",

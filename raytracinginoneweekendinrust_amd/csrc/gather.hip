@@ -12,6 +12,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <string.h>
+
+#include <map>
+#include <mutex>
 #include <string>
 
 #include "../../include/rt.h"
@@ -120,6 +124,95 @@ int rt_shard_unpack(const float* d_packed_all, uint32_t width, uint32_t height, 
                        d_packed_all, width, height, g.bx, g.nb, n, d_image);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? RT_OK : hip_fail(e, "shard_unpack launch");
+}
+
+// Peer transport (frame_gather.FrameGather's "ipc" path): rank 0 exports its gather
+// buffer with hipIpcGetMemHandle, every other rank maps it (hipIpcOpenMemHandle) and copies
+// its packed shard straight into its slot, device to device over xGMI, one hop instead of
+// the D2H + H2D bounce through host memory. The buffer may sit inside a larger allocation
+// (a caching allocator's segment): the handle names the allocation's base and the offset
+// travels in the last 8 bytes of the RT_IPC_HANDLE_BYTES record.
+struct IpcRecord {
+    hipIpcMemHandle_t h;
+    uint64_t offset;
+};
+static_assert(sizeof(IpcRecord) <= RT_IPC_HANDLE_BYTES, "IPC record size");
+namespace {
+std::mutex g_ipc_mu;
+std::map<uintptr_t, void*> g_ipc_base;  // mapped pointer handed out -> base hipIpcOpenMemHandle returned
+struct DevSwitch {
+    int prev = -1;
+    hipError_t e;
+    explicit DevSwitch(int d) {
+        (void)hipGetDevice(&prev);
+        e = hipSetDevice(d);
+    }
+    ~DevSwitch() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+}  // namespace
+
+int rt_ipc_export(const void* d_ptr, int device, uint8_t handle[RT_IPC_HANDLE_BYTES]) {
+    rthost::clear_error();
+    if (!d_ptr || !handle) return rthost::set_error(RT_ERR_INVALID, "rt_ipc_export: NULL argument");
+    DevSwitch ds(device);
+    if (ds.e != hipSuccess) return hip_fail(ds.e, "hipSetDevice");
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+    hipError_t e = hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)d_ptr);
+    if (e != hipSuccess) return hip_fail(e, "hipMemGetAddressRange");
+    IpcRecord rec{};
+    if ((e = hipIpcGetMemHandle(&rec.h, (void*)base)) != hipSuccess) return hip_fail(e, "hipIpcGetMemHandle");
+    rec.offset = (uint64_t)((const char*)d_ptr - (const char*)base);
+    memset(handle, 0, RT_IPC_HANDLE_BYTES);
+    memcpy(handle, &rec, sizeof rec);
+    return RT_OK;
+}
+
+int rt_ipc_open(const uint8_t handle[RT_IPC_HANDLE_BYTES], int device, void** d_ptr) {
+    rthost::clear_error();
+    if (!handle || !d_ptr) return rthost::set_error(RT_ERR_INVALID, "rt_ipc_open: NULL argument");
+    *d_ptr = nullptr;
+    IpcRecord rec;
+    memcpy(&rec, handle, sizeof rec);
+    DevSwitch ds(device);
+    if (ds.e != hipSuccess) return hip_fail(ds.e, "hipSetDevice");
+    void* base = nullptr;
+    hipError_t e = hipIpcOpenMemHandle(&base, rec.h, hipIpcMemLazyEnablePeerAccess);
+    if (e != hipSuccess) return hip_fail(e, "hipIpcOpenMemHandle");
+    void* p = (char*)base + rec.offset;
+    {
+        std::lock_guard<std::mutex> lk(g_ipc_mu);
+        g_ipc_base[(uintptr_t)p] = base;
+    }
+    *d_ptr = p;
+    return RT_OK;
+}
+
+int rt_ipc_close(void* d_ptr, int device) {
+    rthost::clear_error();
+    if (!d_ptr) return RT_OK;
+    void* base = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(g_ipc_mu);
+        auto it = g_ipc_base.find((uintptr_t)d_ptr);
+        if (it == g_ipc_base.end()) return rthost::set_error(RT_ERR_INVALID, "rt_ipc_close: pointer not from rt_ipc_open");
+        base = it->second;
+        g_ipc_base.erase(it);
+    }
+    DevSwitch ds(device);
+    if (ds.e != hipSuccess) return hip_fail(ds.e, "hipSetDevice");
+    hipError_t e = hipIpcCloseMemHandle(base);
+    return e == hipSuccess ? RT_OK : hip_fail(e, "hipIpcCloseMemHandle");
+}
+
+int rt_copy_async(void* d_dst, const void* d_src, uint64_t bytes, void* stream) {
+    rthost::clear_error();
+    if (bytes == 0) return RT_OK;
+    if (!d_dst || !d_src) return rthost::set_error(RT_ERR_INVALID, "rt_copy_async: NULL buffer");
+    hipError_t e = hipMemcpyAsync(d_dst, d_src, bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream);
+    return e == hipSuccess ? RT_OK : hip_fail(e, "hipMemcpyAsync (shard to rank 0)");
 }
 
 }  // extern "C"

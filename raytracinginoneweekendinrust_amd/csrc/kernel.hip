@@ -46,13 +46,6 @@ using rtdev::DevTexture;
 using rtdev::f4;
 
 #define RT_DEV __device__ __forceinline__
-// A/B diagnostic only (tools/session_*.sh variants): N wave-wide VALU instructions that do nothing,
-// to price issue slots at a point of the kernel (compiled out unless RT_PAD_* is defined).
-#define RT_VALU_PAD(N)                                                              \
-    do {                                                                            \
-        float _p = 0.0f;                                                            \
-        _Pragma("unroll") for (int _i = 0; _i < (N); ++_i) asm volatile("v_add_f32 %0, %0, %0" : "+v"(_p)); \
-    } while (0)
 
 namespace {
 
@@ -938,7 +931,6 @@ RT_DEV void sort2(float& ta, uint32_t& ca, float& tb, uint32_t& cb) {  // branch
 // to an axis plane (a zero direction component) gets t = (k - o) / d = 0 / 0 from
 // a rect whose plane holds its origin, and every comparison against NaN passes
 // (rectangle.rs:36-65); its sample is re-traced by the reference kernel.
-[[maybe_unused]] constexpr uint32_t kDeferBit = 0x20000000u;  // a deferred leaf node on the stack (RT_LEAF_DEFER)
 // A BVH traversal's state between visits (bvh_run).
 struct Trav {
     uint32_t cur, sp, best_rank;
@@ -1063,30 +1055,8 @@ RT_DEV bool bvh_run(const DevScene& S, float delta, const f4* wrapper, const Ray
         }
         // One batch of loads per step: a leaf node needs the .xy halves of its
         // rows, an interior node its six box rows and child codes.
-#ifdef RT_LEAF_DEFER
-        // Leaf deferral: a lane about to test a leaf node while fewer than RT_LEAF_DEFER
-        // lanes of the wave are at one (and some are at interior nodes) swaps that node
-        // with its stack top and visits the top entry now; the leaf node, marked
-        // kDeferBit, is tested when popped (never deferred twice, never pop-pruned), so
-        // leaf tests run with more lanes. Visiting a node the pop-time prune would skip
-        // only costs time: every child test is still the reference's.
-        {
-            const bool at_leaf = (cur & (rtdev::kLeafNodeFlag | kDeferBit)) == rtdev::kLeafNodeFlag;
-            const uint32_t nl = (uint32_t)__popcll(__ballot(at_leaf)), na = (uint32_t)__popcll(__ballot(1));
-            if (at_leaf && nl < (uint32_t)RT_LEAF_DEFER && nl < na && sp > 0u &&
-                (!(kF & kFDeep) || sp <= S.stack_depth)) {
-                const uint32_t x = stk[(sp - 1u) * 128u];
-                stk[(sp - 1u) * 128u] = cur | kDeferBit;
-                stk[(sp - 1u) * 128u + 64u] = __float_as_uint(-kInf);
-                cur = x;
-            }
-        }
-        const bool leaf_node = (cur & rtdev::kLeafNodeFlag) != 0u;
-        const uint32_t nbo = (cur & ~(rtdev::kLeafNodeFlag | kDeferBit)) * (rtdev::kBvhNodeF4 * 16u);
-#else
         const bool leaf_node = (cur & rtdev::kLeafNodeFlag) != 0u;
         const uint32_t nbo = (cur & ~rtdev::kLeafNodeFlag) * (rtdev::kBvhNodeF4 * 16u);  // node byte offset
-#endif
         // The near-plane row offsets. The sphere-BVH presets rederive them each trip from the
         // direction's sign bits (volatile asm is not hoisted: three loop-invariant offsets live
         // across the loop, where registers are scarcest, pushed C3's sample-loop state into
@@ -1106,16 +1076,13 @@ RT_DEV bool bvh_run(const DevScene& S, float delta, const f4* wrapper, const Ray
             onz = (msz & 48u) + 32u;
         }
 #ifdef RT_LEAF_AUDIT
-        if ((cur & ~(rtdev::kLeafNodeFlag | kDeferBit)) >= S.num_nodes || sp > S.stack_depth + S.spill_depth) {
+        if ((cur & ~rtdev::kLeafNodeFlag) >= S.num_nodes || sp > S.stack_depth + S.spill_depth) {
             atomicAdd(&g_bounds_audit_count, 1u);
             break;
         }
 #endif
 #ifdef RT_PROFILE_REGIONS
         ++visits;
-#endif
-#ifdef RT_PAD_BVH
-        RT_VALU_PAD(RT_PAD_BVH);
 #endif
         PROF_T0(pt);
         if (leaf_node) {
@@ -1600,12 +1567,7 @@ __device__ __noinline__ double turbulence(const uint8_t* tabs, double px, double
 // two), the requester sums its octaves in fbm_get's order, and only the final
 // perlin3 runs per lane. Every value is the one turbulence() computes, bit for bit.
 // `tab` = the Marble's first permutation table (DevTexture::a).
-#ifdef RT_TURB_NOINLINE
-__device__ __noinline__
-#else
-__device__ __forceinline__
-#endif
-double turbulence_wave(const uint8_t* perm, bool need, V p, uint32_t tab) {
+__device__ __forceinline__ double turbulence_wave(const uint8_t* perm, bool need, V p, uint32_t tab) {
     const uint32_t lane = __lane_id();
     unsigned long long pending = __ballot(need);
     double xd = 0.0, yd = 0.0, zd = 0.0;
@@ -2278,11 +2240,8 @@ constexpr uint32_t kSuspLanes = RT_SUSPEND;  // suspend a BVH traversal's tail a
 // kWaves: the waves per SIMD the register allocator must allow. 3 (<= 168 VGPRs)
 // is the default; the fast kernel also exists at 4 (<= 128 VGPRs, a few spills),
 // launched when the scene's LDS stack fits four waves per SIMD (rt_render_launch).
-#ifndef RT_W4_WAVES
-#define RT_W4_WAVES 4  // A/B diagnostic: the occupancy the "4-wave" instances are compiled for
-#endif
 template <int kKind, int kWaves = 3, uint32_t kF = kFAll>
-__global__ __launch_bounds__(64, kWaves == 4 ? RT_W4_WAVES : kWaves) void trace_samples(DevScene Sg, DevCamera C, DevParams P, ChunkParams Q,
+__global__ __launch_bounds__(64, kWaves) void trace_samples(DevScene Sg, DevCamera C, DevParams P, ChunkParams Q,
                                                     float* __restrict__ sbuf, TraceCounters* __restrict__ ctr,
                                                     ReplayItem* __restrict__ replay_list, uint32_t fixup,
                                                     unsigned long long* __restrict__ seg_counter) {
@@ -2403,9 +2362,6 @@ __global__ __launch_bounds__(64, kWaves == 4 ? RT_W4_WAVES : kWaves) void trace_
         }
         PROF_ADD(kPrRefill, pr);
         if (__ballot(has) == 0ull) break;  // pool exhausted and every path finished
-#ifdef RT_PAD_TRIP
-        RT_VALU_PAD(RT_PAD_TRIP);
-#endif
 #ifdef RT_PROFILE_REGIONS
         if (kKind == 0) {  // throughput histogram: this iteration's segments into the current bucket
             const uint32_t b = (uint32_t)((__builtin_amdgcn_s_memrealtime() - wave_t0) / kTpTicks);
@@ -2689,25 +2645,19 @@ using TraceKernel = void (*)(DevScene, DevCamera, DevParams, ChunkParams, float*
 // come from kernel_mc.hip, compiled with the memory-clause scheduling strategy:
 // measured on the same box it is 1.3% faster on C3 and 1.2% on C2 but 1-2% slower
 // on the other presets (C4, C5), and a scheduling strategy is a per-file flag.
-// Diagnostic builds only (-DRT_SUSP_ALL, A/B of the suspending walk on every preset).
-#ifdef RT_SUSP_ALL
-constexpr uint32_t kSuspAll = kFSusp;
-#else
-constexpr uint32_t kSuspAll = 0u;
-#endif
 // The flat-list instances come from kernel_flat.hip, where philox_block is inlined: the
 // call's register saves cost that preset 8% (C5 151 -> 140 ms per 200-spp frame, same box),
 // while the BVH presets are 1-2% slower with it inlined (C3, C4) and C2 is unchanged.
 template <int kWaves, uint32_t kF>
 TraceKernel preset_instance() {
 #ifdef RT_SPLIT_MC
-    if constexpr (kSuspAll == 0u && kWaves == 4 && (kF == kFBvh || kF == (kFBvh | kFMarble) || kF == kFRuns))
+    if constexpr (kWaves == 4 && (kF == kFBvh || kF == (kFBvh | kFMarble) || kF == kFRuns))
         return reinterpret_cast<TraceKernel>(rt_mc_trace_instance(kF));
-    else if constexpr (kSuspAll == 0u && kF == 0u)
+    else if constexpr (kF == 0u)
         return reinterpret_cast<TraceKernel>(rt_flat_trace_instance(kWaves));
     else
 #endif
-        return trace_samples<0, kWaves, kF | kSuspAll>;
+        return trace_samples<0, kWaves, kF>;
 }
 template <int kWaves>
 TraceKernel fast_instance(uint32_t features) {
@@ -2863,10 +2813,8 @@ int rt_scene_upload(const rt_scene_desc* desc, int device, rt_scene_handle* out)
     d.hrpp_npred = hs.num_predictors;
     s->coord_bound = hs.coord_bound;
     s->features = (hs.tri.empty() ? 0u : kFTri) | (hs.bvh_rect_msph ? kFLeafRM : 0u);
-#ifndef RT_NO_MARBLE_COOP
     for (const rtdev::DevTexture& t : hs.texs)
         if (t.kind == rtdev::kTexMarble) s->features |= kFMarble;
-#endif
 #ifndef RT_LEAF_AUDIT  // (the audit build replays traversals on the same LDS stack: no spill area)
     {  // deep BVHs: the LDS stack keeps kStackLdsMax entries, HBM the rest
         uint32_t cap = kStackLdsMax;

@@ -79,6 +79,7 @@ inline int total_cmp(float a, float b) {  // f32::total_cmp
     return (l > r) - (l < r);
 }
 constexpr float kEps = 1.1920929e-07f;  // f32::EPSILON
+constexpr float kInfF = __builtin_inff();
 
 inline uint32_t fbits(float f) { return rt_spec_f32_bits(f); }
 inline float bitsf(uint32_t u) { return rt_spec_bits_f32(u); }
@@ -540,6 +541,17 @@ class Lowerer {
         }
     }
 
+    // The box a prebuilt tree's leaf slot keeps for the device's conservative leaf
+    // reject (leaf_intervals2_nf; prunable BVHs only). The reference tests only the
+    // caller's node boxes (bvh.rs:363-417) and stores no shutter times (bvh.rs:38-43),
+    // so nothing here may depend on RT_OBJ_BVH_TREE's f[0] / f[1]: a static primitive's
+    // own box (time-independent), and an unbounded box for a moving sphere, whose tree is
+    // never pruned (its f32 quadratic has no error bound), so the reject never reads it.
+    Box leaf_reject_box(const rt_node& c) {
+        if (c.kind == RT_OBJ_MOVING_SPHERE) return {{-kInfF, -kInfF, -kInfF}, {kInfF, kInfF, kInfF}};
+        return prim_box(c, 0.0f, 0.0f);
+    }
+
     // --- BVH ---------------------------------------------------------------
     struct TNode {
         uint32_t child[2];  // temp node index or leaf code
@@ -687,12 +699,12 @@ class Lowerer {
                 int rc;
                 t.is_node[0] = t.is_node[1] = false;
                 if ((rc = lower_prim(obj[0], &t.child[0]))) return rc;
-                t.leaf_box[0] = prim_box(node(obj[0]), n.f[0], n.f[1]);
+                t.leaf_box[0] = leaf_reject_box(node(obj[0]));
                 if (obj[1] == obj[0]) {  // a 1-object node repeats its object: same result tested once
                     t.child[1] = rtdev::kChildEmpty;
                 } else {
                     if ((rc = lower_prim(obj[1], &t.child[1]))) return rc;
-                    t.leaf_box[1] = prim_box(node(obj[1]), n.f[0], n.f[1]);
+                    t.leaf_box[1] = leaf_reject_box(node(obj[1]));
                 }
             } else {
                 const int ch[2] = {b.left, b.right};

@@ -4,9 +4,10 @@ Each rank computes its share with bench.rank_work() exactly as on the GPU box an
 renders it (the CPU oracle stands in for the device here — the GPU path's own
 shard/sample-range semantics are checked bit-exactly in test_gpu_parity.py):
   strong (bench's default): the shards go through the SAME FrameGather the bench
-          runs (shared-memory slots at rt_shard_offset, the gloo barrier, rank 0's
-          assembly), with torch restatements of rt_shard_pack / rt_shard_unpack in
-          place of the HIP kernels (tested on the device in test_gpu_boundary.py);
+          runs (its shared-memory transport: alternating slots at rt_shard_offset, the
+          gloo barrier, rank 0's assembly; three frames back to back), with torch
+          restatements of rt_shard_pack / rt_shard_unpack in place of the HIP kernels
+          (tested on the device in test_gpu_boundary.py);
           rank 0's frame equals the single-process frame bit for bit;
   weak:   the mean of the rank frames equals one render with N*spp samples up to
           float reassociation of the per-pixel sum (rtol 1e-6).
@@ -76,11 +77,20 @@ def _worker(rank, world, port, scaling, q):
             from raytracinginoneweekendinrust_amd.frame_gather import FrameGather
             g = FrameGather(cfg.width, cfg.height, rank, world, "cpu", pack=cpu_pack, unpack=cpu_unpack)
             try:
-                full = g.gather(torch.from_numpy(img).reshape(-1))
+                assert g.transport == "shm"
+                # three frames back to back through the alternating slots: the frame, its
+                # double, the frame again (a step must never read another's shards)
+                outs = []
+                for scale in (1.0, 2.0, 1.0):
+                    full = g.gather(torch.from_numpy(img * np.float32(scale)).reshape(-1))
+                    if rank == 0:
+                        outs.append(full.numpy().reshape(1, cfg.height, cfg.width, 3).copy())
+                    else:
+                        assert full is None
                 if rank == 0:
-                    q.put((full.numpy().reshape(1, cfg.height, cfg.width, 3).copy(), cnt["seconds"]))
-                else:
-                    assert full is None
+                    np.testing.assert_array_equal(outs[1], outs[0] * np.float32(2.0))
+                    np.testing.assert_array_equal(outs[2], outs[0])
+                    q.put((outs[0], cnt["seconds"]))
             finally:
                 g.close()
             return

@@ -34,6 +34,22 @@ def test_prebuilt_tree_and_camera_basis_match_oracle(rt, orc, tree):
     assert st["segments"] == cnt["segments"]
 
 
+def test_prebuilt_tree_with_moving_spheres_ignores_tree_times(rt, orc):
+    """A caller's Bvh stores no shutter times (bvh.rs:38-43): a tree of spheres, cubes and
+    moving spheres handed over with f[0] = f[1] = 0 renders exactly like the oracle, which
+    tests only the caller's node boxes (leaf rejects must not use those times)."""
+    scene = sphere_scene(rt, n=60, seed=23, tree="median-x", moving=40, tree_times=(0.0, 0.0))
+    p = rt.render_params(64, 40, 8, 10, background=(0.7, 0.8, 1.0))
+    ds = rt.DeviceScene(scene)
+    try:
+        got, st = ds.render(_cam(rt), p)
+    finally:
+        ds.close()
+    want, cnt = orc.render(scene, _cam(rt), p)
+    np.testing.assert_array_equal(got, want)
+    assert st["segments"] == cnt["segments"]
+
+
 def test_camera_basis_equals_camera_new_on_device(rt):
     cfg = rt.CONFIGS["C3"].scaled(48, 4)
     scene = rt.Scene.generate(cfg.scene, cfg.scene_seed)

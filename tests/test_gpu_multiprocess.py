@@ -45,3 +45,18 @@ def test_two_rank_bench_gathers_the_one_gpu_frame():
     assert two["frame_sum"] == one["frame_sum"]
     assert two["image_finite"] and one["image_finite"]
     assert two["rays_per_s"] > 0
+    assert two["config"]["gather"] in ("ipc", "shm")
+
+
+def test_two_rank_bench_back_to_back_frames_over_both_transports():
+    """Three frames through the gather's alternating slots (warmup 1 + 2 timed steps) over
+    the peer (IPC) transport and over the /dev/shm bounce: rank 0 ends with the one-GPU
+    frame bit for bit either way."""
+    common = ["--config", "C1", "--steps", "2", "--warmup", "1", "--no-cpu-baseline"]
+    one = _bench(common, (sys.executable,))
+    for transport in ("ipc", "shm"):
+        two = _bench(["--gpus", "2", "--gather", transport, *common],
+                     (sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                      "--master-addr", "127.0.0.1", "--master-port", str(_port())))
+        assert two["config"]["gather"] == transport
+        assert two["frame_sum"] == one["frame_sum"], transport

@@ -14,6 +14,13 @@ def prim_box(kind: int, f) -> tuple:
     eps = np.float32(1.1920929e-07)
     if kind == K.RT_OBJ_SPHERE:
         return tuple(f[:3] - f[3]), tuple(f[:3] + f[3])
+    if kind == K.RT_OBJ_MOVING_SPHERE:  # bounding_box(0, 1), moving_sphere.rs:86-93 (end_box.min at time_0)
+        c0, c1, t0, t1, r = f[:3], f[3:6], f[6], f[7], f[8]
+
+        def center(t):
+            return c0 + np.float32((np.float32(t) - t0) / (t1 - t0)) * (c1 - c0)
+        a, b = center(0.0), center(1.0)
+        return tuple(np.minimum(a - r, a - r)), tuple(np.maximum(a + r, b + r))
     if kind == K.RT_OBJ_CUBE:
         return tuple(f[:3]), tuple(f[3:6])
     if kind == K.RT_OBJ_TRI:
@@ -66,8 +73,9 @@ def build_tree(rt, objs, boxes, rng, split="random"):
     return nodes, root
 
 
-def sphere_scene(rt, n=120, seed=5, tree="random", with_tree=True, cubes=20):
-    """Ground + n spheres (+ cubes) in a prebuilt tree (or a flat list when not with_tree)."""
+def sphere_scene(rt, n=120, seed=5, tree="random", with_tree=True, cubes=20, moving=0, tree_times=(0.0, 1.0)):
+    """Ground + n spheres (+ cubes, + `moving` moving spheres) in a prebuilt tree (or a flat
+    list when not with_tree); `tree_times` are the f[0] / f[1] the tree node is given."""
     rng = np.random.default_rng(seed)
     b = rt.SceneBuilder()
     world = rt.HittableList()
@@ -89,9 +97,16 @@ def sphere_scene(rt, n=120, seed=5, tree="random", with_tree=True, cubes=20):
         f = (float(x), 0.0, float(z), float(x) + s, 2 * s, float(z) + s)
         objs.append(b.cube(f[:3], f[3:], b.lambertian_from_color(tuple(rng.uniform(0, 1, 3)))))
         boxes.append(prim_box(K.RT_OBJ_CUBE, f))
+    for i in range(moving):
+        x, z = rng.uniform(-9, 9, 2)
+        r = float(rng.uniform(0.15, 0.3))
+        c0 = (float(x), r, float(z))
+        c1 = (float(x), r + float(rng.uniform(0.1, 0.5)), float(z))
+        objs.append(b.moving_sphere(c0, c1, 0.0, 1.0, r, b.lambertian_from_color(tuple(rng.uniform(0, 1, 3)))))
+        boxes.append(prim_box(K.RT_OBJ_MOVING_SPHERE, (*c0, *c1, 0.0, 1.0, r)))
     if with_tree:
         nodes, root = build_tree(rt, objs, boxes, rng, tree)
-        world.add(b.bvh_tree(nodes, root))
+        world.add(b.bvh_tree(nodes, root, *tree_times))
     else:
         for o in objs:
             world.add(o)
