@@ -276,6 +276,7 @@ def main() -> int:
                        "gather": gather.transport if gather is not None else None,
                        "exact_bvh": args.exact_bvh},
             "rays_per_s": seg_total / wall_max,
+            "segments": int(seg_total),
             "segments_per_sample": seg_total / total_samples if total_samples else None,
             "image_finite": img_ok,
             "frame_sum": frame_sum,

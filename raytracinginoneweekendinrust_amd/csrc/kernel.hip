@@ -80,6 +80,9 @@ constexpr uint32_t kModePruneAllExp = 1u << 20;
 // 8: C3 69.7 -> 68.0 ms, C1 -3%). BlocksForward (RT_OPT_TUNE, A/B only) restores
 // the top-first order. Either order gives the same bits (samples are keyed by pixel and index).
 constexpr uint32_t kModeBlocksForward = 1u << 21;
+// NoPool (RT_OPT_TUNE at rt_scene_upload; A/B and tests): the sphere-BVH + Marble preset without the
+// cross-wave traversal pool (kFPool), one wave per workgroup like every other instance.
+constexpr uint32_t kModeNoPool = 1u << 22;
 #ifdef RT_ABLATE
 // Ablation build (librtamd_ablate.so, diagnostics only): RT_OPT_TUNE bits that run a
 // piece of work twice (results of the copy discarded through an opaque test),
@@ -131,10 +134,10 @@ __device__ __forceinline__ void prof_flush() {
 __device__ __forceinline__ void prof_add(uint32_t region, uint64_t t0) {
     uint64_t dt = __builtin_amdgcn_s_memtime() - t0;
     uint64_t m = __ballot(1);
-    if (__lane_id() == (uint32_t)__builtin_ctzll(m)) {
-        prof_lds[region] += dt;
-        prof_lds[kPrCount + region] += 1u;
-        prof_lds[2 * kPrCount + region] += (uint64_t)__popcll(m);
+    if (__lane_id() == (uint32_t)__builtin_ctzll(m)) {  // atomics: a kFPool workgroup's waves share prof_lds
+        atomicAdd(&prof_lds[region], (unsigned long long)dt);
+        atomicAdd(&prof_lds[kPrCount + region], 1ull);
+        atomicAdd(&prof_lds[2 * kPrCount + region], (unsigned long long)__popcll(m));
     }
 }
 #define PROF_INIT() prof_init()
@@ -486,6 +489,42 @@ constexpr uint32_t kFBvh = 1u, kFTri = 2u, kFRuns = 4u, kFDeep = 8u, kFLeafRM = 
 // are 5-8% slower with it (C3 124 -> 133 ms, C5 152 -> 160 ms), so only that preset uses it.
 constexpr uint32_t kFSusp = 64u;
 [[maybe_unused]] constexpr uint32_t kStackLdsMax = 19u;  // LDS stack entries per lane at most (9.5 KB per wave: 16 waves/CU)
+// kFPool (a strategy, like kFSusp): the cross-wave traversal pool. A kFPool instance runs in
+// workgroups of kPoolWaves waves that share their LDS. At a top-level BVH entry each wave
+// traverses until at most kPoolPost of its lanes are still traversing; those lanes then post
+// their traversal state (ray, 1/d, t range, best candidate, next node, stack depth, stack
+// owner) into the workgroup's pool. After a barrier the first wave to claim the pool runs every
+// posted traversal to its end, refilling its lanes from the pool as they finish (a traversal's
+// stack stays in its owner's LDS column / HBM spill slab, Trav::sid), and writes the results
+// back; after a second barrier each owner takes its result. A traversal's node visits, leaf
+// tests and their order are exactly the ones its owner would have made (only the lane that
+// executes them changes), so the bits are the same; the traversal tails, which ran at a few
+// lanes in each of four waves (C3: 11-17 lanes per BVH trip), run together in one wave, and
+// the waiting waves leave their SIMDs' issue slots to other workgroups.
+constexpr uint32_t kFPool = 128u;
+constexpr uint32_t kPoolWaves = 4u;     // waves per workgroup of a kFPool instance
+constexpr uint32_t kPoolPost = 16u;     // a wave posts its traversals once this few lanes still traverse
+constexpr uint32_t kPoolCap = kPoolWaves * kPoolPost;  // items per pool
+constexpr uint32_t kPoolWords = 17u;    // LDS words per item (structure of arrays: word w of item i at w * kPoolCap + i)
+constexpr uint32_t kPoolRefill = 48u;   // the processing wave refills its lanes once this few are still busy
+constexpr uint32_t kPoolPerWave = 48u;  // posted items per processing wave
+[[maybe_unused]] constexpr uint32_t kPoolStackLds = 14u; // LDS stack entries per lane in kFPool instances (entries past it: HBM)
+// pool area: two pools (consecutive calls alternate, so a fast wave posting into the next call's
+// pool never meets a slow wave still reading this call's results) + 4 counters each (n, take, claim)
+// + two sets of kPoolWaves loop votes (pool_live)
+constexpr uint32_t kPoolLdsWords = 2u * kPoolWords * kPoolCap + 16u;
+// The sample loop of a kFPool workgroup ends for all its waves together: every wave keeps meeting
+// the pool's barriers (with no active lanes) until none of them has work, so no barrier is ever
+// left waiting for a wave that has ended. One barrier per trip: the votes alternate between two sets.
+[[maybe_unused]] RT_DEV bool pool_live(uint32_t* lds, uint32_t stack_region, bool live, uint32_t wave, uint32_t lane, uint32_t& trip) {
+    uint32_t* votes = lds + kPoolWaves * stack_region + 2u * kPoolWords * kPoolCap + 8u + (trip & 1u) * kPoolWaves;
+    trip += 1u;
+    if (lane == 0u) votes[wave] = live ? 1u : 0u;
+    __syncthreads();
+    uint32_t any = 0u;
+    for (uint32_t w = 0; w < kPoolWaves; ++w) any |= votes[w];
+    return any != 0u;
+}
 // One leaf (primitive or cube). tmax = closest so far; a hit with t == closest is
 // accepted, so later candidates win ties exactly like hittable.rs:110-116.
 template <uint32_t kF = kFAll>
@@ -931,12 +970,16 @@ RT_DEV void sort2(float& ta, uint32_t& ca, float& tb, uint32_t& cb) {  // branch
 // to an axis plane (a zero direction component) gets t = (k - o) / d = 0 / 0 from
 // a rect whose plane holds its origin, and every comparison against NaN passes
 // (rectangle.rs:36-65); its sample is re-traced by the reference kernel.
-// A BVH traversal's state between visits (bvh_run).
+// A BVH traversal's state between visits (bvh_run). sid: the global thread id (wave * 64 + lane)
+// of the lane that owns the traversal's stack (its LDS column and, for deep stacks, its HBM spill
+// slab): the lane itself, or another wave's lane whose traversal it took over (kFPool).
 struct Trav {
     uint32_t cur, sp, best_rank;
     float tmax_entry;
     bool any;
+    uint32_t sid;
 };
+RT_DEV uint32_t self_sid() { return blockIdx.x * blockDim.x + threadIdx.x; }
 // Audit build: every completed fast traversal is replayed with the reference recursion
 // (bvh_hit_reference, on the lane's now free LDS stack); disagreements are recorded.
 RT_DEV void trav_audit(const DevScene& S, const f4* wrapper, uint32_t root, const Ray& r, V inv, float tmin,
@@ -1009,7 +1052,7 @@ RT_DEV bool bvh_hit(const DevScene& S, float delta, uint32_t root, const Ray& r,
         }
     }
     PROF_ADD(kPrBvhSetup, psetup);
-    Trav tv{root, 0u, 0u, closest, false};
+    Trav tv{root, 0u, 0u, closest, false, self_sid()};
     bvh_run<kKind, kF, false>(S, delta, wrapper, r, inv, tmin, closest, hit_code, stk, mode, tv, 0u);
     const bool any = tv.any;
     PROF_ADD(kPrBvhCall, pcall);
@@ -1040,6 +1083,7 @@ RT_DEV bool bvh_run(const DevScene& S, float delta, const f4* wrapper, const Ray
                                     hnz = inv.z < 0.0f ? 80u : 32u;
     bool any = tv.any;
     uint32_t best_rank = tv.best_rank, sp = tv.sp, cur = tv.cur;
+    [[maybe_unused]] const uint32_t sid = tv.sid;
     bool finished = true;
     [[maybe_unused]] uint32_t trips = 0;
 #ifdef RT_PROFILE_REGIONS
@@ -1199,7 +1243,7 @@ RT_DEV bool bvh_run(const DevScene& S, float delta, const f4* wrapper, const Ray
                 stk[sp * 128u + 64u] = __float_as_uint(t);
             } else {
                 uint32_t* g = S.stack_spill +
-                              (((size_t)blockIdx.x * S.spill_depth + (sp - S.stack_depth)) * 64u + threadIdx.x) * 2u;
+                              (((size_t)(sid >> 6) * S.spill_depth + (sp - S.stack_depth)) * 64u + (sid & 63u)) * 2u;
                 g[0] = node;
                 g[1] = __float_as_uint(t);
             }
@@ -1225,7 +1269,7 @@ RT_DEV bool bvh_run(const DevScene& S, float delta, const f4* wrapper, const Ray
                 tenter = __uint_as_float(stk[sp * 128u + 64u]);
             } else {
                 const uint32_t* g = S.stack_spill +
-                                    (((size_t)blockIdx.x * S.spill_depth + (sp - S.stack_depth)) * 64u + threadIdx.x) * 2u;
+                                    (((size_t)(sid >> 6) * S.spill_depth + (sp - S.stack_depth)) * 64u + (sid & 63u)) * 2u;
                 cand = g[0];
                 tenter = __uint_as_float(g[1]);
             }
@@ -1238,7 +1282,7 @@ RT_DEV bool bvh_run(const DevScene& S, float delta, const f4* wrapper, const Ray
         PROF_ADD(kPrBvhPop, ppop);
         if (!found) break;
     }
-    tv = Trav{cur, sp, best_rank, tmax_entry, any};
+    tv = Trav{cur, sp, best_rank, tmax_entry, any, sid};
 #ifdef RT_PROFILE_REGIONS
     {
         const uint32_t b = trips_bin(visits);
@@ -1250,9 +1294,9 @@ RT_DEV bool bvh_run(const DevScene& S, float delta, const f4* wrapper, const Ray
         const uint32_t first = (uint32_t)__builtin_ctzll(__ballot(1));
         for (uint32_t bin = 0; bin < 8u; ++bin) {
             const uint32_t n = (uint32_t)__popcll(__ballot(b == bin));
-            if (__lane_id() == first && n) prof_lds[3u * kPrCount + bin] += n;
+            if (__lane_id() == first && n) atomicAdd(&prof_lds[3u * kPrCount + bin], (unsigned long long)n);
         }
-        if (__lane_id() == first) prof_lds[3u * kPrCount + 8u + trips_bin(m)] += 1u;
+        if (__lane_id() == first) atomicAdd(&prof_lds[3u * kPrCount + 8u + trips_bin(m)], 1ull);
     }
 #endif
     return finished;
@@ -1840,6 +1884,194 @@ RT_DEV bool world_hit(const DevScene& S, float delta, const Ray& r, Rng& g, cons
     return any;
 }
 
+// One top-level BVH entry (hittable.rs:110-116 for a Bvh, bvh.rs:212-217, 363-417) through the
+// workgroup's traversal pool (kFPool, above). Called by every wave of the workgroup, in uniform
+// control flow, for the same entry in the same order (world_hit_pool); `active` lanes have a ray.
+// closest / hit_code / any_out are the lane's walk state, updated like entry_geom_hit does.
+template <uint32_t kF>
+RT_DEV void bvh_pool(const DevScene& S, float delta, const DevEntry* E, const Ray& ray, bool active, float& closest,
+                     uint32_t& hit_code, bool& any_out, uint32_t* lds, uint32_t* stk, uint32_t lane, uint32_t& call,
+                     uint32_t mode, bool& replay) {
+    const uint32_t root = E->payload;
+    const f4* wrapper = S.nodes + (size_t)root * rtdev::kBvhNodeF4;
+    Ray r = ray;
+    const uint32_t ntf = E->ntf;
+    for (uint32_t i = 0; i < ntf; ++i) r = apply_op(E->tf[i], r);
+    const V inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
+    bool mine = false;
+    if (active) {  // bvh_hit's hand-over rule (NaN-prone rays go to the reference kernel)
+        const float ax = __builtin_fabsf(inv.x), ay = __builtin_fabsf(inv.y), az = __builtin_fabsf(inv.z);
+        const bool fast = ax > 0.0f && ax < kInf && ay > 0.0f && ay < kInf && az > 0.0f && az < kInf &&
+                          __builtin_fabsf(r.o.x) < kInf && __builtin_fabsf(r.o.y) < kInf && __builtin_fabsf(r.o.z) < kInf;
+        if (!fast) replay = true;
+        mine = fast;
+    }
+    const uint32_t region = S.stack_depth * 128u;  // LDS words of one wave's stack
+    uint32_t* pool = lds + kPoolWaves * region;
+    const uint32_t par = call & 1u;
+    uint32_t* P = pool + par * (kPoolWords * kPoolCap);
+    uint32_t* ctr = pool + 2u * kPoolWords * kPoolCap + 4u * par;  // n, take, claim
+    call += 1u;
+    Trav tv{root, 0u, 0u, closest, false, self_sid()};
+    bool post = false;
+    if (mine) {  // phase 1: the wave's own traversals, until at most kPoolPost lanes still traverse
+        if (bvh_run<0, kF, true>(S, delta, wrapper, r, inv, 0.001f, closest, hit_code, stk, mode, tv, kPoolPost)) {
+            trav_audit(S, wrapper, root, r, inv, 0.001f, tv, closest, hit_code, stk);
+            any_out = tv.any;
+        } else {
+            post = true;
+        }
+    }
+    const unsigned long long pm = __ballot(post);
+    uint32_t slot = 0u;
+    if (pm) {
+        uint32_t base = 0u;
+        if (lane == 0u) base = atomicAdd(&ctr[0], (uint32_t)__popcll(pm));
+        base = __builtin_amdgcn_readfirstlane(base);
+        slot = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(pm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)pm, 0u));
+    }
+    if (post) {
+        uint32_t* q = P + slot;
+        q[0 * kPoolCap] = __float_as_uint(r.o.x);
+        q[1 * kPoolCap] = __float_as_uint(r.o.y);
+        q[2 * kPoolCap] = __float_as_uint(r.o.z);
+        q[3 * kPoolCap] = __float_as_uint(r.d.x);
+        q[4 * kPoolCap] = __float_as_uint(r.d.y);
+        q[5 * kPoolCap] = __float_as_uint(r.d.z);
+        q[6 * kPoolCap] = __float_as_uint(inv.x);
+        q[7 * kPoolCap] = __float_as_uint(inv.y);
+        q[8 * kPoolCap] = __float_as_uint(inv.z);
+        q[9 * kPoolCap] = __float_as_uint(r.time);
+        q[10 * kPoolCap] = __float_as_uint(tv.tmax_entry);
+        q[11 * kPoolCap] = __float_as_uint(closest);
+        q[12 * kPoolCap] = hit_code;
+        q[13 * kPoolCap] = tv.best_rank | (tv.any ? 0x80000000u : 0u);
+        q[14 * kPoolCap] = tv.cur;
+        q[15 * kPoolCap] = tv.sp;
+        q[16 * kPoolCap] = tv.sid;
+    }
+    __syncthreads();
+    const uint32_t n = ctr[0];
+    uint32_t claim = ~0u;
+    if (n != 0u) {
+        if (lane == 0u) claim = atomicAdd(&ctr[2], 1u);
+        claim = __builtin_amdgcn_readfirstlane(claim);
+        if (claim < (n + kPoolPerWave - 1u) / kPoolPerWave) {
+            // phase 2: this wave runs posted traversals, each lane taking the next item when free
+            bool busy = false;
+            uint32_t item = 0u, phit = 0u;
+            float pclose = 0.0f;
+            Ray pr{};
+            V pinv = mk(0.0f, 0.0f, 0.0f);
+            Trav ptv{};
+            uint32_t* pstk = stk;
+            for (;;) {
+                const unsigned long long idle = __ballot(!busy);
+                uint32_t t0 = 0u;
+                if (idle) {
+                    if (lane == 0u) t0 = atomicAdd(&ctr[1], (uint32_t)__popcll(idle));
+                    t0 = __builtin_amdgcn_readfirstlane(t0);
+                }
+                if (!busy) {
+                    const uint32_t it =
+                        t0 + __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
+                    if (it < n) {
+                        const uint32_t* q = P + it;
+                        pr.o = mk(__uint_as_float(q[0 * kPoolCap]), __uint_as_float(q[1 * kPoolCap]),
+                                  __uint_as_float(q[2 * kPoolCap]));
+                        pr.d = mk(__uint_as_float(q[3 * kPoolCap]), __uint_as_float(q[4 * kPoolCap]),
+                                  __uint_as_float(q[5 * kPoolCap]));
+                        pinv = mk(__uint_as_float(q[6 * kPoolCap]), __uint_as_float(q[7 * kPoolCap]),
+                                  __uint_as_float(q[8 * kPoolCap]));
+                        pr.time = __uint_as_float(q[9 * kPoolCap]);
+                        pclose = __uint_as_float(q[11 * kPoolCap]);
+                        phit = q[12 * kPoolCap];
+                        const uint32_t br = q[13 * kPoolCap];
+                        ptv = Trav{q[14 * kPoolCap], q[15 * kPoolCap], br & 0x7fffffffu, __uint_as_float(q[10 * kPoolCap]),
+                                   (br >> 31) != 0u, q[16 * kPoolCap]};
+                        // the owner's stack column: wave (sid >> 6) & 3 of this workgroup, lane sid & 63
+                        pstk = lds + ((ptv.sid >> 6) & (kPoolWaves - 1u)) * region + (ptv.sid & 63u);
+                        item = it;
+                        busy = true;
+                    }
+                }
+                if (__ballot(busy) == 0ull) break;
+                const bool more = t0 + (uint32_t)__popcll(idle) < n;  // items still in the pool
+                if (busy) {
+                    if (bvh_run<0, kF, true>(S, delta, wrapper, pr, pinv, 0.001f, pclose, phit, pstk, mode, ptv,
+                                             more ? kPoolRefill : 0u)) {
+                        trav_audit(S, wrapper, root, pr, pinv, 0.001f, ptv, pclose, phit, pstk);
+                        uint32_t* q = P + item;
+                        q[11 * kPoolCap] = __float_as_uint(pclose);
+                        q[12 * kPoolCap] = phit;
+                        q[13 * kPoolCap] = ptv.best_rank | (ptv.any ? 0x80000000u : 0u);
+                        busy = false;
+                    }
+                }
+            }
+        }
+    }
+    __syncthreads();
+    if (post) {  // phase 3: the owner takes its traversal's result
+        const uint32_t* q = P + slot;
+        closest = __uint_as_float(q[11 * kPoolCap]);
+        hit_code = q[12 * kPoolCap];
+        any_out = (q[13 * kPoolCap] >> 31) != 0u;
+    }
+    // the first claimer (alive: it just passed both barriers) clears this pool's counters for
+    // their next use two calls on; every read of them happened before the second barrier, and the
+    // next post into this pool follows the next call's first barrier
+    if (claim == 0u && lane == 0u) {
+        ctr[0] = 0u;
+        ctr[1] = 0u;
+        ctr[2] = 0u;
+    }
+}
+
+// HittableList::hit over the world (hittable.rs:100-118) for kFPool instances: world_hit, with
+// every top-level BVH entry going through bvh_pool. Every wave calls it each sample-loop trip
+// (uniform control flow; `active` lanes have a segment to trace), so the waves of a workgroup
+// meet the same pool calls in the same order.
+template <uint32_t kF>
+RT_DEV bool world_hit_pool(const DevScene& S, float delta, const Ray& r, bool active, Rng& g, const Key& k,
+                           float& t_hit, uint32_t& hit_entry, uint32_t& hit_code, uint32_t* lds, uint32_t* stk,
+                           uint32_t lane, uint32_t& call, uint32_t mode, bool& replay) {
+    float closest = kInf;
+    bool any = false;
+    for (uint32_t e = 0; e < S.num_top; ++e) {
+        const DevEntry* E = S.entries + e;
+        if (E->kind == rtdev::kEntBvh) {
+            bool h = false;
+            uint32_t code = hit_code;
+            bvh_pool<kF>(S, delta, E, r, active, closest, code, h, lds, stk, lane, call, mode, replay);
+            if (h) {
+                hit_entry = e;
+                hit_code = code;
+                any = true;
+            }
+        } else if (active) {
+            if (E->kind == rtdev::kEntMedium) {
+                float t;
+                if (medium_hit<0, kF>(S, delta, E, r, 0.001f, closest, g, k, t, stk, mode, replay)) {
+                    closest = t;
+                    hit_entry = e;
+                    hit_code = rtdev::leaf_code(rtdev::kLeafMedium, 0);
+                    any = true;
+                }
+            } else {
+                uint32_t code;
+                if (entry_geom_hit<0, kF>(S, delta, E, r, 0.001f, closest, code, stk, mode, replay)) {
+                    hit_entry = e;
+                    hit_code = code;
+                    any = true;
+                }
+            }
+        }
+    }
+    t_hit = closest;
+    return any;
+}
+
 // The suspending list walk of the fast kernel (instances with kFSusp): hittable.rs:100-118 per lane from
 // its own position. A lane's walk state survives the trips of the sample loop: when a BVH
 // traversal is suspended (bvh_run<.., true>: at most `susp` lanes of the wave were left in
@@ -1889,7 +2121,7 @@ RT_DEV void world_walk(const DevScene& S, float delta, const Ray& ray, Rng& g, c
                     w.pos = S.num_top + 1u;  // abandoned: the sample is re-traced by the reference kernel
                     continue;
                 }
-                w.tv = Trav{root, 0u, 0u, w.closest, false};
+                w.tv = Trav{root, 0u, 0u, w.closest, false, self_sid()};
             }
             if (bvh_run<0, kF, true>(S, delta, wrapper, r, inv, 0.001f, w.closest, w.hit_code, stk, mode, w.tv, susp)) {
                 trav_audit(S, wrapper, root, r, inv, 0.001f, w.tv, w.closest, w.hit_code, stk);
@@ -2001,6 +2233,7 @@ RT_DEV bool take_sample(ItemPool& pool, bool want, const DevCamera& C, const Dev
                         uint32_t lane, uint32_t& slot, uint32_t& s_local, V& L, V& T, uint32_t& depth, Rng& g,
                         Ray& ray) {
     bool got = false;
+    const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);  // waves of the launch
     for (;;) {
         unsigned long long need = __ballot(want && !got);
         if (need == 0ull || pool.exhausted) break;
@@ -2017,7 +2250,7 @@ RT_DEV bool take_sample(ItemPool& pool, bool want, const DevCamera& C, const Dev
                 if (lane == 0u) {
                     const uint32_t n = __hip_atomic_load(&ctr->replay_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     const uint32_t pl = __hip_atomic_load(&ctr->replay_pull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    lim += (n > pl ? n - pl : 0u) / gridDim.x;
+                    lim += (n > pl ? n - pl : 0u) / nwaves;
                 }
                 lim = __builtin_amdgcn_readfirstlane(lim);
                 if (64u - (uint32_t)__popcll(need) >= lim) break;
@@ -2030,13 +2263,13 @@ RT_DEV bool take_sample(ItemPool& pool, bool want, const DevCamera& C, const Dev
                     role_event(bt);
 #endif
                 } else if (list) {  // a share of the list per wave: a replayed path runs with few others
-                    cnt = (list_n + gridDim.x - 1u) / gridDim.x;
+                    cnt = (list_n + nwaves - 1u) / nwaves;
                     cnt = cnt > 64u ? 64u : cnt;
                     bt = atomicAdd(counter, cnt);
                 } else {
                     const uint32_t cur = __hip_atomic_load(counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     const uint32_t rem = cur < Q.units ? Q.units - cur : 0u;
-                    cnt = rem / (Q.guide * gridDim.x);
+                    cnt = rem / (Q.guide * nwaves);
                     cnt = cnt < 1u ? 1u : (cnt > Q.group ? Q.group : cnt);
                     bt = atomicAdd(counter, cnt);
                 }
@@ -2241,17 +2474,26 @@ constexpr uint32_t kSuspLanes = RT_SUSPEND;  // suspend a BVH traversal's tail a
 // is the default; the fast kernel also exists at 4 (<= 128 VGPRs, a few spills),
 // launched when the scene's LDS stack fits four waves per SIMD (rt_render_launch).
 template <int kKind, int kWaves = 3, uint32_t kF = kFAll>
-__global__ __launch_bounds__(64, kWaves) void trace_samples(DevScene Sg, DevCamera C, DevParams P, ChunkParams Q,
+__global__ __launch_bounds__((kF & kFPool) != 0u ? 64u * kPoolWaves : 64u, kWaves) void trace_samples(DevScene Sg, DevCamera C, DevParams P, ChunkParams Q,
                                                     float* __restrict__ sbuf, TraceCounters* __restrict__ ctr,
                                                     ReplayItem* __restrict__ replay_list, uint32_t fixup,
                                                     unsigned long long* __restrict__ seg_counter) {
     extern __shared__ uint32_t lds_stack[];
-    const uint32_t lane = threadIdx.x;
-    uint32_t* stk = lds_stack + lane;  // [level][{node, t_enter}][lane]
+    // kFPool instances run kPoolWaves waves per workgroup (one stack region per wave, then the
+    // pool); every other instance one wave per workgroup
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    DevScene S = Sg;
+    uint32_t* stk = lds_stack + wave * S.stack_depth * 128u + lane;  // [level][{node, t_enter}][lane]
+    [[maybe_unused]] uint32_t pool_call = 0u;  // kFPool: top-level BVH calls so far (the same in every wave)
+    [[maybe_unused]] uint32_t pool_trip = 0u;  // kFPool: sample-loop trips so far (the same in every wave)
+    if constexpr ((kF & kFPool) != 0u) {
+        if (threadIdx.x < 16u) lds_stack[kPoolWaves * S.stack_depth * 128u + 2u * kPoolWords * kPoolCap + threadIdx.x] = 0u;
+        __syncthreads();
+    }
     // Perlin permutation tables (Marble) behind the stack when they fit: the
     // three dependent byte lookups per lattice corner then hit LDS, not L2.
-    DevScene S = Sg;
-    if (S.perm_bytes != 0u && S.perm_bytes <= kPermLdsMax && !(P.tune & kModeNoPermLds)) {
+    if (!(kF & kFPool) && S.perm_bytes != 0u && S.perm_bytes <= kPermLdsMax && !(P.tune & kModeNoPermLds)) {
         uint32_t* tab = lds_stack + S.stack_depth * 128u;
         const uint32_t* src = reinterpret_cast<const uint32_t*>(Sg.perm);
         for (uint32_t i = lane; i < S.perm_bytes / 4u; i += 64u) tab[i] = src[i];
@@ -2361,7 +2603,11 @@ __global__ __launch_bounds__(64, kWaves) void trace_samples(DevScene Sg, DevCame
             has = true;
         }
         PROF_ADD(kPrRefill, pr);
-        if (__ballot(has) == 0ull) break;  // pool exhausted and every path finished
+        if constexpr ((kF & kFPool) != 0u) {  // the workgroup's waves end together (pool_live)
+            if (!pool_live(lds_stack, S.stack_depth * 128u, __ballot(has) != 0ull, wave, lane, pool_trip)) break;
+        } else if (__ballot(has) == 0ull) {
+            break;  // pool exhausted and every path finished
+        }
 #ifdef RT_PROFILE_REGIONS
         if (kKind == 0) {  // throughput histogram: this iteration's segments into the current bucket
             const uint32_t b = (uint32_t)((__builtin_amdgcn_s_memrealtime() - wave_t0) / kTpTicks);
@@ -2373,7 +2619,33 @@ __global__ __launch_bounds__(64, kWaves) void trace_samples(DevScene Sg, DevCame
             tp_acc += (uint32_t)__popcll(__ballot(has));
         }
 #endif
-        if constexpr ((kF & kFMarble) != 0u) {
+        if constexpr ((kF & kFPool) != 0u) {  // every wave walks the world, active lanes with a segment
+            bool replay = false, any = false;
+            float t = 0.0f;
+            uint32_t he = 0, hc = 0;
+            PROF_T0(pw);
+            any = world_hit_pool<kF>(S, P.prune_delta, ray, has, g, k, t, he, hc, lds_stack, stk, lane, pool_call,
+                                     mode, replay);
+            PROF_ADD(kPrWorld, pw);
+            bool shade = has;
+            if (has && replay) {  // hand the sample to the reference kernel
+                unsigned idx = atomicAdd(&ctr->replay_count, 1u);
+                if (idx < kReplayCap) replay_publish(replay_list, idx, g.pixel, g.sample - Q.sample0);
+                has = false;
+                shade = false;
+            }
+            if constexpr ((kF & kFMarble) != 0u) {
+                if (shade_marble<kF>(S, P, Q, k, sbuf, shade, any, he, hc, t, ray, L, T, depth, g, slot,
+                                     g.sample - Q.sample0)) {
+                    has = false;
+                    nseg += P.max_depth - depth + (depth != 0u ? 1u : 0u);
+                }
+            } else if (shade && finish_segment<kF>(S, P, Q, k, sbuf, any, he, hc, t, ray, L, T, depth, g, slot,
+                                                   g.sample - Q.sample0)) {
+                has = false;
+                nseg += P.max_depth - depth + (depth != 0u ? 1u : 0u);
+            }
+        } else if constexpr ((kF & kFMarble) != 0u) {
             bool shade = false, any = false;
             float t = 0.0f;
             uint32_t he = 0, hc = 0;
@@ -2427,13 +2699,16 @@ __global__ __launch_bounds__(64, kWaves) void trace_samples(DevScene Sg, DevCame
         __threadfence();  // (release: its replay-list entries and replay_count increments first)
         atomicAdd(&ctr->fast_done, 1u);
     }
+#ifdef RT_PROFILE_REGIONS
+    if constexpr ((kF & kFPool) != 0u) __syncthreads();  // every wave of the workgroup has counted
+#endif
     PROF_FLUSH();
 #ifdef RT_PROFILE_REGIONS
     if (kKind == 0 && lane == 0u && tp_acc && tp_bucket < kTpBuckets) atomicAdd(&g_tp_hist[tp_bucket], tp_acc);
     if (stream_grid && lane == 0u) role_event(0xfffffffeu);
-    if (kKind == 0 && lane == 0u && blockIdx.x < kProfWaves) {
-        g_wave_t[2u * blockIdx.x] = wave_t0;
-        g_wave_t[2u * blockIdx.x + 1u] = __builtin_amdgcn_s_memrealtime();
+    if (kKind == 0 && lane == 0u && (self_sid() >> 6) < kProfWaves) {
+        g_wave_t[2u * (self_sid() >> 6)] = wave_t0;
+        g_wave_t[2u * (self_sid() >> 6) + 1u] = __builtin_amdgcn_s_memrealtime();
     }
 #endif
 }
@@ -2538,6 +2813,10 @@ __global__ void kat_eval(int op, const float* __restrict__ in, float* __restrict
 void* rt_mc_trace_instance(uint32_t preset) {
     if (preset == kFBvh) return reinterpret_cast<void*>(trace_samples<0, 4, kFBvh>);
     if (preset == (kFBvh | kFMarble)) return reinterpret_cast<void*>(trace_samples<0, 4, kFBvh | kFMarble>);
+    if (preset == (kFBvh | kFMarble | kFPool))
+        return reinterpret_cast<void*>(trace_samples<0, 4, kFBvh | kFMarble | kFPool>);
+    if (preset == (kFBvh | kFMarble | kFPool | kFDeep))
+        return reinterpret_cast<void*>(trace_samples<0, 4, kFBvh | kFMarble | kFPool | kFDeep>);
     if (preset == kFRuns) return reinterpret_cast<void*>(trace_samples<0, 4, kFRuns>);
     return nullptr;
 }
@@ -2651,7 +2930,8 @@ using TraceKernel = void (*)(DevScene, DevCamera, DevParams, ChunkParams, float*
 template <int kWaves, uint32_t kF>
 TraceKernel preset_instance() {
 #ifdef RT_SPLIT_MC
-    if constexpr (kWaves == 4 && (kF == kFBvh || kF == (kFBvh | kFMarble) || kF == kFRuns))
+    if constexpr (kWaves == 4 && (kF == kFBvh || kF == (kFBvh | kFMarble) || kF == (kFBvh | kFMarble | kFPool) ||
+                                  kF == (kFBvh | kFMarble | kFPool | kFDeep) || kF == kFRuns))
         return reinterpret_cast<TraceKernel>(rt_mc_trace_instance(kF));
     else if constexpr (kF == 0u)
         return reinterpret_cast<TraceKernel>(rt_flat_trace_instance(kWaves));
@@ -2664,6 +2944,11 @@ TraceKernel fast_instance(uint32_t features) {
     if (features == 0u) return preset_instance<kWaves, 0u>();
     if ((features & ~kFRuns) == 0u) return preset_instance<kWaves, kFRuns>();
     if ((features & ~kFBvh) == 0u) return preset_instance<kWaves, kFBvh>();
+    if constexpr (kWaves == 4) {  // the traversal pool (kFPool) instances of the sphere-BVH + Marble preset
+        if (features == (kFBvh | kFMarble | kFPool)) return preset_instance<4, kFBvh | kFMarble | kFPool>();
+        if (features == (kFBvh | kFMarble | kFPool | kFDeep))
+            return preset_instance<4, kFBvh | kFMarble | kFPool | kFDeep>();
+    }
     if ((features & ~(kFBvh | kFMarble)) == 0u) return preset_instance<kWaves, kFBvh | kFMarble>();
     if ((features & ~(kFBvh | kFTri | kFDeep)) == 0u) return preset_instance<kWaves, kFBvh | kFTri | kFDeep | kFSusp>();
     return preset_instance<kWaves, kFAll>();
@@ -2815,9 +3100,17 @@ int rt_scene_upload(const rt_scene_desc* desc, int device, rt_scene_handle* out)
     s->features = (hs.tri.empty() ? 0u : kFTri) | (hs.bvh_rect_msph ? kFLeafRM : 0u);
     for (const rtdev::DevTexture& t : hs.texs)
         if (t.kind == rtdev::kTexMarble) s->features |= kFMarble;
+    for (const rtdev::DevEntry& e : hs.entries) {  // top-level entries and medium boundaries
+        if (e.kind == rtdev::kEntBvh) s->features |= kFBvh;
+        if (e.kind == rtdev::kEntSphereRun && e.pad[0] >= kRunPretestMin) s->features |= kFRuns;
+    }
+    // the sphere-BVH + Marble preset (showcase) traverses through the workgroup pool (kFPool)
+    // unless RT_OPT_TUNE's kModeNoPool (A/B, tests) says otherwise
+    const bool pool = s->features == (kFBvh | kFMarble) && !(opt(RT_OPT_TUNE) & kModeNoPool);
+    if (pool) s->features |= kFPool;
 #ifndef RT_LEAF_AUDIT  // (the audit build replays traversals on the same LDS stack: no spill area)
-    {  // deep BVHs: the LDS stack keeps kStackLdsMax entries, HBM the rest
-        uint32_t cap = kStackLdsMax;
+    {  // deep BVHs: the LDS stack keeps kStackLdsMax entries (kPoolStackLds in pool instances), HBM the rest
+        uint32_t cap = pool ? kPoolStackLds : kStackLdsMax;
         if (const int64_t v = opt(RT_OPT_STACK_LDS))  // diagnostics / tests: a smaller LDS part (>= 1)
             cap = std::min(cap, (uint32_t)v);
         if (hs.max_stack > cap) {
@@ -2827,10 +3120,6 @@ int rt_scene_upload(const rt_scene_desc* desc, int device, rt_scene_handle* out)
         }
     }
 #endif
-    for (const rtdev::DevEntry& e : hs.entries) {  // top-level entries and medium boundaries
-        if (e.kind == rtdev::kEntBvh) s->features |= kFBvh;
-        if (e.kind == rtdev::kEntSphereRun && e.pad[0] >= kRunPretestMin) s->features |= kFRuns;
-    }
     uint64_t c[10] = {hs.entries.size(), hs.sph.size(), hs.msph.size() / 3, hs.rect.size() / 2, hs.tri.size() / 3,
                       hs.nodes.size() / rtdev::kBvhNodeF4, hs.mats.size(), hs.texs.size(), hs.max_bvh_depth, total};
     memcpy(s->counts, c, sizeof c);
@@ -3138,14 +3427,19 @@ int rt_render_launch_camera(rt_scene_handle s, const rt_camera* camera, const rt
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per3, k3, 64, stack_lds + perm3) != hipSuccess) per3 = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per4, k4, 64, stack_lds) != hipSuccess) per4 = 0;
         s->fast_waves = per4 > per3 && !(dp.tune & kModeW3) && !prefer3 ? 4 : 3;
+        if (s->features & kFPool) s->fast_waves = 4;  // (pool instances exist at four waves per SIMD)
     }
+    // kFPool instances run kPoolWaves waves per workgroup: their stacks, then the pool
+    const bool pool = (s->features & kFPool) != 0u;
+    const uint32_t wg_waves = pool ? kPoolWaves : 1u;
     if (s->fast_waves == 4) dp.tune |= kModeNoPermLds;
     // LDS per wave: the kernel's traversal stack, then the Perlin tables
     DevScene dev_ref = s->dev;
     dev_ref.stack_depth = s->stack_ref;
     const size_t perm_lds =
         s->dev.perm_bytes != 0u && s->dev.perm_bytes <= kPermLdsMax && !(dp.tune & kModeNoPermLds) ? s->dev.perm_bytes : 0u;
-    const size_t lds = (size_t)s->dev.stack_depth * 128u * sizeof(uint32_t) + perm_lds;
+    const size_t lds = pool ? kPoolWaves * (size_t)s->dev.stack_depth * 128u * sizeof(uint32_t) + kPoolLdsWords * 4u
+                            : (size_t)s->dev.stack_depth * 128u * sizeof(uint32_t) + perm_lds;
     size_t lds_ref = (size_t)dev_ref.stack_depth * 128u * sizeof(uint32_t) + perm_lds;
     if ((dp.flags & RT_FLAG_HRPP) && s->dev.hrpp_npred) {  // the experiment: reference kernel + predictors
         dp.flags |= RT_FLAG_EXACT_BVH;
@@ -3174,9 +3468,10 @@ int rt_render_launch_camera(rt_scene_handle s, const rt_camera* camera, const rt
     if (s->grid == 0) {
         int per_cu = 0, per_cu_ref = 0, cus = 0;
         const TraceKernel kf = fast_instance(s->fast_waves, s->features);
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kf, 64, lds) != hipSuccess ||
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kf, 64 * wg_waves, lds) != hipSuccess ||
             per_cu < 1)
-            per_cu = 8;
+            per_cu = 8 / (int)wg_waves;
+        per_cu *= (int)wg_waves;  // resident waves per CU
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_ref, trace_samples<1>, 64, lds_ref) != hipSuccess ||
             per_cu_ref < 1)
             per_cu_ref = 8;
@@ -3215,7 +3510,8 @@ int rt_render_launch_camera(rt_scene_handle s, const rt_camera* camera, const rt
         uint32_t grid = (uint32_t)s->grid, grid_ref = (uint32_t)s->grid_ref;
         if (grid > q.units) grid = q.units;
         if (grid_ref > q.units) grid_ref = q.units;
-        q.fast_grid = grid;
+        const uint32_t fast_blocks = (grid + wg_waves - 1u) / wg_waves;  // workgroups of the fast kernel
+        q.fast_grid = exact || dev_ref.hrpp_tab ? grid : fast_blocks * wg_waves;  // its waves
         hipEvent_t* evp = nullptr;
         if (s->ev_count < rt_scene::kEvents) {
             evp = s->ev[s->ev_count];
@@ -3237,8 +3533,8 @@ int rt_render_launch_camera(rt_scene_handle s, const rt_camera* camera, const rt
             const bool kind3 = !(s->features & kFDeep) && !(dp.tune & kModeReplayRef);
             const bool stream_rp = kind3 && !(dp.tune & kModeNoStream);
             if (stream_rp && (e = hipEventRecord(s->fork, st)) != hipSuccess) return hip_fail(e, "replay stream fork");
-            hipLaunchKernelGGL(kf, dim3(grid), dim3(64), lds, st, s->dev, cam, dp, q, s->sbuf, s->counter, s->replay,
-                               0u, d_segments);
+            hipLaunchKernelGGL(kf, dim3(fast_blocks), dim3(64 * wg_waves), lds, st, s->dev, cam, dp, q, s->sbuf,
+                               s->counter, s->replay, 0u, d_segments);
             if (kind3) {
                 // the replay pass: fast traversal except for the rays that were handed over
                 DevScene dev_rp = s->dev;

@@ -23,11 +23,21 @@ from raytracinginoneweekendinrust_amd import _capi  # noqa: E402  (structs only)
 from raytracinginoneweekendinrust_amd.configs import CONFIGS  # noqa: E402
 
 
-def bind(path):
-    lib = C.CDLL(path)
+def bind(spec, idx):
+    """spec: path.so, or path.so:0xTUNE (that library's RT_OPT_TUNE bits, e.g. 0x400000 = no traversal
+    pool). Each spec loads its own copy of the file, so one build can be compared with itself."""
+    import shutil
+    import tempfile
+    path, _, tune = spec.partition(":")
+    copy = os.path.join(tempfile.gettempdir(), f"ab_{os.getpid()}_{idx}_{os.path.basename(path)}")
+    shutil.copyfile(path, copy)
+    lib = C.CDLL(copy)
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import rtopts
     rtopts.apply_lib(lib)
+    if tune:
+        lib.rt_set_option.argtypes = [C.c_int, C.c_int64]
+        lib.rt_set_option(0, int(tune, 0))
     lib.rt_scene_generate.argtypes = [C.c_char_p, C.c_uint64, C.c_char_p, C.POINTER(C.POINTER(_capi.rt_scene_desc))]
     lib.rt_scene_upload.argtypes = [C.POINTER(_capi.rt_scene_desc), C.c_int, C.POINTER(C.c_void_p)]
     lib.rt_render.argtypes = [C.c_void_p, C.POINTER(_capi.rt_camera_desc), C.POINTER(_capi.rt_render_params),
@@ -51,8 +61,8 @@ def main():
     params = rt.render_params(cfg.width, cfg.height, cfg.spp, cfg.depth, background=cfg.background(),
                               seed=cfg.render_seed)
     ref = None
-    for path in a.libs:
-        lib = bind(path)
+    for i, path in enumerate(a.libs):
+        lib = bind(path, i)
         desc = C.POINTER(_capi.rt_scene_desc)()
         assert lib.rt_scene_generate(cfg.scene.encode(), cfg.scene_seed, _capi.ASSET_DIR.encode(), C.byref(desc)) == 0
         h = C.c_void_p()
@@ -70,7 +80,7 @@ def main():
         if ref is None:
             ref = img.copy()
         samples = cfg.width * cfg.height * cfg.spp
-        print(f"{os.path.basename(path):28s} {med:9.1f} ms  {samples / med / 1e3:8.1f} Msamples/s  "
+        print(f"{os.path.basename(path):40s} {med:9.1f} ms  {samples / med / 1e3:8.1f} Msamples/s  "
               f"segments {segs}  image {same}", flush=True)
         lib.rt_scene_free(h)
 

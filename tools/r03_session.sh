@@ -64,6 +64,28 @@ first)  # round start: GPU suite, smoke, bench, calibration, C3 dual-issue count
     pmc "c3_valu2" SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VALU2 SQ_THREAD_CYCLES_VALU SQ_BUSY_CYCLES \
         SQ_WAVE_CYCLES GRBM_GUI_ACTIVE -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline
     ;;
+probe)  # dual-issue rules, the C3 region profile and instruction classes of the current kernel
+    step valu_rate_w4 600 tools/valu_rate all 4
+    step valu_rate_w2 600 tools/valu_rate all 2
+    for c in v_max_f32 v_cndmask_b32_e32 v_and_b32 v_mov_b32 v_cmp_lt_f32_e32; do
+        pmc "$c" SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VALU2 SQ_THREAD_CYCLES_VALU GRBM_GUI_ACTIVE \
+            -- tools/valu_rate $c 4 30
+    done
+    step regions_c3 600 env RT_LIBRARY=raytracinginoneweekendinrust_amd/_lib/librtamd_prof.so \
+        python3 tools/region_profile.py --config C3 --spp 64
+    B="python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline"
+    pmc c3_mix1 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_TRANS_F32 \
+        SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_CVT SQ_INSTS_VALU_INT64 SQ_INSTS_VALU -- $B
+    pmc c3_mix2 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 \
+        SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VALU -- $B
+    ;;
+pool)  # the traversal pool: its parity test, the GPU suite, A/B against the one-wave instance
+    step pool_test 600 python -u -m pytest tests/test_gpu_parity.py -x -v --timeout 300 --timeout-method thread \
+        -k "traversal_pool"
+    L=raytracinginoneweekendinrust_amd/_lib/librtamd.so
+    step ab_c3 900 python -u tools/ab_time.py --config C3 --spp 100 --reps 3 $L $L:0x400000 $L $L:0x400000
+    gpu_tests
+    ;;
 ab)  # A/B of library builds: bash tools/r03_session.sh ab <config> <spp> lib1.so lib2.so ...
     CFG="$1"; SPP="$2"; shift 2
     step "ab_$CFG" 900 python -u tools/ab_time.py --config "$CFG" --spp "$SPP" --reps 3 "$@"
