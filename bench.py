@@ -97,15 +97,16 @@ def pmc_summary(kind: str, cfg_name: str, md5: str):
 SUBSAMPLE = 64  # counts from a fixed 1/64 subsample at the config's spp and depth
 
 
-def oracle_measure(cfg, scene, threads: int):
+def oracle_measure(cfg, scene, threads: int, full: bool = False):
     """Oracle render of the fixed 1/64 block subsample (8x8 blocks b with
-    b % 64 == 21, spread over the whole frame) at full spp/depth: the CPU baseline
-    (Msamples/s on `threads` host threads) and the reference algorithm's per-sample
-    counts for the roofline's algorithmic bytes."""
+    b % 64 == 21, spread over the whole frame) at full spp/depth, or of the whole frame
+    (`full`): the CPU baseline (Msamples/s on `threads` host threads) and the reference
+    algorithm's per-sample counts for the roofline's algorithmic bytes."""
     import oracle_ffi as orc
     import raytracinginoneweekendinrust_amd as rt
-    p = rt.render_params(cfg.width, cfg.height, cfg.spp, cfg.depth, background=cfg.background(), shard_index=21,
-                         shard_count=SUBSAMPLE, seed=cfg.render_seed)
+    shard = {} if full else {"shard_index": 21, "shard_count": SUBSAMPLE}
+    p = rt.render_params(cfg.width, cfg.height, cfg.spp, cfg.depth, background=cfg.background(),
+                         seed=cfg.render_seed, **shard)
     _, cnt = orc.render(scene, cfg.camera(), p, threads=threads)
     return cnt
 
@@ -137,6 +138,9 @@ def main() -> int:
     ap.add_argument("--config", default="C3")
     ap.add_argument("--scaling", choices=["weak", "strong"], default="strong")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=None,
+                    help="oracle threads for cpu_baseline (default: the box's CPU share; C1: 1, as BASELINE config 1 "
+                         "states, over the whole frame)")
     ap.add_argument("--exact-bvh", action="store_true")
     ap.add_argument("--gather", choices=["auto", "ipc", "shm"], default="auto",
                     help="N>1 frame gather transport (frame_gather.FrameGather)")
@@ -224,19 +228,22 @@ def main() -> int:
     frame_sum = float(frame[0].double().sum().item()) if rank == 0 and frame[0] is not None else None
 
     if rank == 0:
-        threads = cpu_threads()
+        # BASELINE.json config 1 (C1) is the single-thread CPU reference over the whole frame
+        c1 = cfg.name == "C1" and args.cpu_threads is None
+        threads = 1 if c1 else (args.cpu_threads or cpu_threads())
         cpu = None
         try:
-            cnt = oracle_measure(cfg, scene, threads)
+            cnt = oracle_measure(cfg, scene, threads, full=c1)
             if world == 1 and not args.no_cpu_baseline:
                 cpu = {"value": cnt["samples"] / cnt["seconds"] / 1e6, "unit": "Msamples/s", "cores": cnt["threads"],
                        "kind": "port", "label": "oracle restatement (C, pthreads)", "host_nproc": host_nproc(),
                        "note": "the C oracle restatement of the reference (oracle/oracle.c), the Rust reference "
                                "cannot be built here; threads = the affinity mask capped by OMP_NUM_THREADS "
                                "(the box's CPU share)",
-                       "sample": f"{cfg.name} 8x8 blocks b % {SUBSAMPLE} == 21 ({cnt['samples'] // spp} px, 1/64 of "
-                                 f"the frame) at {spp} spp depth {cfg.depth}: {cnt['samples']} samples in "
-                                 f"{cnt['seconds']:.1f}s (C oracle, pthreads)"}
+                       "sample": (f"{cfg.name} whole frame ({cnt['samples'] // spp} px)" if c1 else
+                                  f"{cfg.name} 8x8 blocks b % {SUBSAMPLE} == 21 ({cnt['samples'] // spp} px, 1/64 of "
+                                  f"the frame)") + f" at {spp} spp depth {cfg.depth}: {cnt['samples']} samples in "
+                                 f"{cnt['seconds']:.1f}s (C oracle, {cnt['threads']} thread(s))"}
         except Exception as e:  # the oracle is optional on the box; the product path is not
             log(f"oracle unavailable: {e}")
             cnt = None

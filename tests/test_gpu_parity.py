@@ -268,10 +268,11 @@ def test_c3_full_resolution_one_spp_matches_oracle(rt, orc):
     np.testing.assert_array_equal(got, want)
 
 
-@pytest.mark.parametrize("cfg_name,shard", [("C3", 101), ("C4", 77), ("C5", 200)])
+@pytest.mark.parametrize("cfg_name,shard", [("C2", 137), ("C3", 101), ("C4", 77), ("C5", 200)])
 def test_full_workload_subsample_matches_oracle(cfg_name, shard, rt, orc):
-    # the full-size render on the GPU (C3 1200x800x500, C4 1920x1080x1000 over the
-    # 20k-triangle mesh, C5 1920x1080x2000 with the media), checked bit-exactly on a
+    # the full-size render on the GPU (C2 1200x800x500 over the 485-sphere list with the f32
+    # pretest, C3 1200x800x500, C4 1920x1080x1000 over the 20k-triangle mesh, C5 1920x1080x2000
+    # with the media), checked bit-exactly on a
     # 1/256 block shard rendered by the oracle at the same full spp and depth
     cfg = rt.CONFIGS[cfg_name]
     scene = rt.Scene.generate(cfg.scene, cfg.scene_seed)

@@ -26,11 +26,15 @@ pytestmark = pytest.mark.gpu
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 STATS = json.load(open(os.path.join(HERE, "golden", "reference_image_stats.json")))
-# lights_and_marble.png is not what the current simple_lights scene (src/main.rs:377-401)
-# renders: the oracle gives a u8 mean of 0.077 linear (0.137 even with a gamma-2 curve) against
-# the image's 0.239 — its floor is lit far more evenly, so it predates the scene's present
-# light setup (the README never cites it). It is reported, not asserted.
-STALE = {"lights_and_marble": "image predates the current simple_lights light setup (u8 mean 0.24 vs 0.08)"}
+# lights_and_marble.png shows the simple_lights geometry (src/main.rs:377-401) under the book
+# camera — the sphere light, the marble sphere and the edge-on XyRect light sit at the oracle
+# render's pixel positions — but not its light: main.rs:393's emission 4 gives a u8 mean of 0.079
+# (0.148 with a gamma-2 curve) against the image's 0.239, and tests/golden/lights_and_marble_search.py
+# finds the image's mean and histogram at emission 16 with gamma 2 (mean 0.246, histogram TV 0.06)
+# or emission 32 linear (0.245, TV 0.08): the image was rendered with 4-8x brighter lights than the
+# source holds. Reported, not asserted.
+STALE = {"lights_and_marble": "image rendered with 4-8x the emission of main.rs:393 (tests/golden/"
+                              "lights_and_marble_search.py: emission 16 + gamma 2 matches mean 0.246 vs 0.239, TV 0.06)"}
 SPP = {"showcase": 256, "smoke": 512, "motion_blur": 128, "spheres_render_checkered": 128, "lights_and_marble": 512}
 
 
