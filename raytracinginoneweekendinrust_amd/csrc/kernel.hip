@@ -80,9 +80,10 @@ constexpr uint32_t kModePruneAllExp = 1u << 20;
 // 8: C3 69.7 -> 68.0 ms, C1 -3%). BlocksForward (RT_OPT_TUNE, A/B only) restores
 // the top-first order. Either order gives the same bits (samples are keyed by pixel and index).
 constexpr uint32_t kModeBlocksForward = 1u << 21;
-// NoPool (RT_OPT_TUNE at rt_scene_upload; A/B and tests): the sphere-BVH + Marble preset without the
-// cross-wave traversal pool (kFPool), one wave per workgroup like every other instance.
-constexpr uint32_t kModeNoPool = 1u << 22;
+// Pool (RT_OPT_TUNE at rt_scene_upload; A/B and tests): the sphere-BVH + Marble preset through the
+// cross-wave traversal pool (kFPool) instead of the one-wave instance. Bit-exact, and slower: C3 at
+// 100 spp 102 ms without, 192-209 ms with it (profiles/r03/pool/), so it is not the default.
+constexpr uint32_t kModePool = 1u << 22;
 #ifdef RT_ABLATE
 // Ablation build (librtamd_ablate.so, diagnostics only): RT_OPT_TUNE bits that run a
 // piece of work twice (results of the copy discarded through an opaque test),
@@ -172,6 +173,25 @@ __device__ unsigned g_bounds_audit_count;
 __device__ TravAudit g_trav_audit[kAuditMax];
 #endif
 
+#ifdef RT_POOL_CHECK
+// Diagnostic build (-DRT_POOL_CHECK): consistency checks of the traversal pool (kFPool); a violation
+// is counted and the offending item dropped (no fault), and the counts are printed at rt_scene_free.
+// Build: make single NAME=pc VFLAGS=-DRT_POOL_CHECK; run: RT_LIBRARY=../_lib/librtamd_pc.so pytest
+// tests/test_gpu_parity.py -k pool. [0] item taken with an invalid state ([5] node, [6] stack depth,
+// [7] owner out of range), [1] owner collected another traversal's item, [2] owner collected a
+// result with an invalid hit code, [3] items served, [4] items served by a wave other than their
+// owner, [8] / [9] ready / done bits already set at posting, [10] a taken bit already cleared,
+// [11] a taken item already done, [13] an LDS stack push past stack_depth. (This build found the
+// sign-extended ready mask, bvh_pool's ready_all.)
+__device__ unsigned g_pool_check[16];
+// the first anomaly of a run: (type << 24) | (block << 2) | wave
+__device__ unsigned g_pool_first;
+RT_DEV void pool_anomaly(uint32_t type, uint32_t wave) {
+    atomicAdd(&g_pool_check[type], 1u);
+    atomicCAS(&g_pool_first, 0u, (type << 24) | (blockIdx.x << 2) | wave);
+}
+__device__ unsigned g_pool_dump[24];
+#endif
 // ---------------------------------------------------------------------------
 // vector math, glam 0.22 evaluation order
 // ---------------------------------------------------------------------------
@@ -490,41 +510,35 @@ constexpr uint32_t kFBvh = 1u, kFTri = 2u, kFRuns = 4u, kFDeep = 8u, kFLeafRM = 
 constexpr uint32_t kFSusp = 64u;
 [[maybe_unused]] constexpr uint32_t kStackLdsMax = 19u;  // LDS stack entries per lane at most (9.5 KB per wave: 16 waves/CU)
 // kFPool (a strategy, like kFSusp): the cross-wave traversal pool. A kFPool instance runs in
-// workgroups of kPoolWaves waves that share their LDS. At a top-level BVH entry each wave
-// traverses until at most kPoolPost of its lanes are still traversing; those lanes then post
-// their traversal state (ray, 1/d, t range, best candidate, next node, stack depth, stack
-// owner) into the workgroup's pool. After a barrier the first wave to claim the pool runs every
-// posted traversal to its end, refilling its lanes from the pool as they finish (a traversal's
-// stack stays in its owner's LDS column / HBM spill slab, Trav::sid), and writes the results
-// back; after a second barrier each owner takes its result. A traversal's node visits, leaf
-// tests and their order are exactly the ones its owner would have made (only the lane that
-// executes them changes), so the bits are the same; the traversal tails, which ran at a few
-// lanes in each of four waves (C3: 11-17 lanes per BVH trip), run together in one wave, and
-// the waiting waves leave their SIMDs' issue slots to other workgroups.
+// workgroups of kPoolWaves waves that share their LDS. At a top-level BVH entry each wave traverses
+// until at most kPoolPost of its lanes are still traversing; those lanes post their traversal state
+// (ray, 1/d, t range, best candidate, next node, stack depth, stack owner) into the workgroup's pool,
+// and the wave holding the pool's token runs posted traversals in its idle lanes, refilling them as
+// traversals finish (a traversal's stack stays in its owner's LDS column / HBM spill slab,
+// Trav::sid), while a posting wave that finds the token taken sleeps until its items are done
+// (bvh_pool). A traversal's node visits, leaf tests and their order are exactly the ones its owner
+// would have made (only the lane that executes them changes), so the bits are the same; traversal
+// tails that ran at a few lanes in several waves (C3: 11-17 lanes per BVH trip) run together in one.
+// No barrier: the waves of a workgroup never wait for one another except for posted items.
 constexpr uint32_t kFPool = 128u;
 constexpr uint32_t kPoolWaves = 4u;     // waves per workgroup of a kFPool instance
-constexpr uint32_t kPoolPost = 16u;     // a wave posts its traversals once this few lanes still traverse
-constexpr uint32_t kPoolCap = kPoolWaves * kPoolPost;  // items per pool
-constexpr uint32_t kPoolWords = 17u;    // LDS words per item (structure of arrays: word w of item i at w * kPoolCap + i)
-constexpr uint32_t kPoolRefill = 48u;   // the processing wave refills its lanes once this few are still busy
-constexpr uint32_t kPoolPerWave = 48u;  // posted items per processing wave
-[[maybe_unused]] constexpr uint32_t kPoolStackLds = 14u; // LDS stack entries per lane in kFPool instances (entries past it: HBM)
-// pool area: two pools (consecutive calls alternate, so a fast wave posting into the next call's
-// pool never meets a slow wave still reading this call's results) + 4 counters each (n, take, claim)
-// + two sets of kPoolWaves loop votes (pool_live)
-constexpr uint32_t kPoolLdsWords = 2u * kPoolWords * kPoolCap + 16u;
-// The sample loop of a kFPool workgroup ends for all its waves together: every wave keeps meeting
-// the pool's barriers (with no active lanes) until none of them has work, so no barrier is ever
-// left waiting for a wave that has ended. One barrier per trip: the votes alternate between two sets.
-[[maybe_unused]] RT_DEV bool pool_live(uint32_t* lds, uint32_t stack_region, bool live, uint32_t wave, uint32_t lane, uint32_t& trip) {
-    uint32_t* votes = lds + kPoolWaves * stack_region + 2u * kPoolWords * kPoolCap + 8u + (trip & 1u) * kPoolWaves;
-    trip += 1u;
-    if (lane == 0u) votes[wave] = live ? 1u : 0u;
-    __syncthreads();
-    uint32_t any = 0u;
-    for (uint32_t w = 0; w < kPoolWaves; ++w) any |= votes[w];
-    return any != 0u;
-}
+#ifndef RT_POOL_POST
+#define RT_POOL_POST 16
+#endif
+constexpr uint32_t kPoolPost = RT_POOL_POST;  // a wave posts its traversals once this few lanes still traverse
+constexpr uint32_t kPoolCap = kPoolWaves * kPoolPost;  // item slots: kPoolPost per wave (<= 64: the ready mask)
+static_assert(kPoolCap <= 64u && kPoolPost <= 32u, "ready / done masks: one 32-bit word per wave, 64 slots");
+constexpr uint32_t kPoolWords = 18u;    // LDS words per item (structure of arrays: word w of item i at w * kPoolCap + i)
+#ifndef RT_POOL_REFILL
+#define RT_POOL_REFILL 48
+#endif
+constexpr uint32_t kPoolRefill = RT_POOL_REFILL;  // the server refills its lanes once this few are still busy
+#ifndef RT_POOL_STACK
+#define RT_POOL_STACK 19
+#endif
+[[maybe_unused]] constexpr uint32_t kPoolStackLds = RT_POOL_STACK;  // LDS stack entries per lane (more: HBM)
+// pool area: the items, then per wave a ready and a done mask word, then the server token
+constexpr uint32_t kPoolLdsWords = kPoolWords * kPoolCap + 2u * kPoolWaves + 1u;
 // One leaf (primitive or cube). tmax = closest so far; a hit with t == closest is
 // accepted, so later candidates win ties exactly like hittable.rs:110-116.
 template <uint32_t kF = kFAll>
@@ -1238,6 +1252,9 @@ RT_DEV bool bvh_run(const DevScene& S, float delta, const f4* wrapper, const Ray
         sort2(t1, c1, t2, c2);
         // LDS stack; with kFDeep the entries past stack_depth go to the HBM spill area
         auto push = [&](uint32_t node, float t) {
+#ifdef RT_POOL_CHECK
+            if ((kF & kFPool) && !(kF & kFDeep) && sp >= S.stack_depth) pool_anomaly(13, 0u);
+#endif
             if (!(kF & kFDeep) || sp < S.stack_depth) {
                 stk[sp * 128u] = node;
                 stk[sp * 128u + 64u] = __float_as_uint(t);
@@ -1885,12 +1902,19 @@ RT_DEV bool world_hit(const DevScene& S, float delta, const Ray& r, Rng& g, cons
 }
 
 // One top-level BVH entry (hittable.rs:110-116 for a Bvh, bvh.rs:212-217, 363-417) through the
-// workgroup's traversal pool (kFPool, above). Called by every wave of the workgroup, in uniform
-// control flow, for the same entry in the same order (world_hit_pool); `active` lanes have a ray.
+// workgroup's traversal pool (kFPool, above); no barrier: the waves of a workgroup stay independent.
+// Phase 1: the wave traverses until at most kPoolPost of its lanes are still traversing. Those lanes
+// post their state into the wave's own kPoolPost item slots and set their bits in the workgroup's
+// `ready` mask. Phase 2: one wave at a time is the pool's server (an LDS token): it takes ready items
+// into its idle lanes (its own, and any other wave's posted meanwhile) and runs them, refilling lanes
+// as traversals finish; a finished item's result goes back to its slot and its bit into `done`. A
+// posting wave that finds a server at work sleeps until its items are done; one that finds none
+// becomes the server. The server hands the token back once no item is ready and none of its lanes is
+// busy, and a waiting wave whose items are still ready takes it, so every posted item is served.
 // closest / hit_code / any_out are the lane's walk state, updated like entry_geom_hit does.
 template <uint32_t kF>
 RT_DEV void bvh_pool(const DevScene& S, float delta, const DevEntry* E, const Ray& ray, bool active, float& closest,
-                     uint32_t& hit_code, bool& any_out, uint32_t* lds, uint32_t* stk, uint32_t lane, uint32_t& call,
+                     uint32_t& hit_code, bool& any_out, uint32_t* lds, uint32_t* stk, uint32_t wave, uint32_t lane,
                      uint32_t mode, bool& replay) {
     const uint32_t root = E->payload;
     const f4* wrapper = S.nodes + (size_t)root * rtdev::kBvhNodeF4;
@@ -1906,12 +1930,6 @@ RT_DEV void bvh_pool(const DevScene& S, float delta, const DevEntry* E, const Ra
         if (!fast) replay = true;
         mine = fast;
     }
-    const uint32_t region = S.stack_depth * 128u;  // LDS words of one wave's stack
-    uint32_t* pool = lds + kPoolWaves * region;
-    const uint32_t par = call & 1u;
-    uint32_t* P = pool + par * (kPoolWords * kPoolCap);
-    uint32_t* ctr = pool + 2u * kPoolWords * kPoolCap + 4u * par;  // n, take, claim
-    call += 1u;
     Trav tv{root, 0u, 0u, closest, false, self_sid()};
     bool post = false;
     if (mine) {  // phase 1: the wave's own traversals, until at most kPoolPost lanes still traverse
@@ -1923,13 +1941,17 @@ RT_DEV void bvh_pool(const DevScene& S, float delta, const DevEntry* E, const Ra
         }
     }
     const unsigned long long pm = __ballot(post);
-    uint32_t slot = 0u;
-    if (pm) {
-        uint32_t base = 0u;
-        if (lane == 0u) base = atomicAdd(&ctr[0], (uint32_t)__popcll(pm));
-        base = __builtin_amdgcn_readfirstlane(base);
-        slot = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(pm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)pm, 0u));
-    }
+    if (pm == 0ull) return;
+    const uint32_t region = S.stack_depth * 128u;  // LDS words of one wave's stack
+    uint32_t* P = lds + kPoolWaves * region;       // items: word w of slot i at P[w * kPoolCap + i]
+    // per wave w (32-bit LDS words; bit b = slot w * kPoolPost + b): ready[w] = posted, not yet taken;
+    // done[w] = result written back; then the server token (0 = free, w + 1 = wave w serves)
+    uint32_t* ready = P + kPoolWords * kPoolCap;
+    uint32_t* done = ready + kPoolWaves;
+    uint32_t* token = done + kPoolWaves;
+    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(pm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)pm, 0u));
+    const uint32_t slot = wave * kPoolPost + rank;
+    const uint32_t own = (1u << (uint32_t)__popcll(pm)) - 1u;  // this wave's posted slots in its words
     if (post) {
         uint32_t* q = P + slot;
         q[0 * kPoolCap] = __float_as_uint(r.o.x);
@@ -1949,33 +1971,87 @@ RT_DEV void bvh_pool(const DevScene& S, float delta, const DevEntry* E, const Ra
         q[14 * kPoolCap] = tv.cur;
         q[15 * kPoolCap] = tv.sp;
         q[16 * kPoolCap] = tv.sid;
+        q[17 * kPoolCap] = root;  // waves run asynchronously: the server may be at another entry
     }
-    __syncthreads();
-    const uint32_t n = ctr[0];
-    uint32_t claim = ~0u;
-    if (n != 0u) {
-        if (lane == 0u) claim = atomicAdd(&ctr[2], 1u);
-        claim = __builtin_amdgcn_readfirstlane(claim);
-        if (claim < (n + kPoolPerWave - 1u) / kPoolPerWave) {
-            // phase 2: this wave runs posted traversals, each lane taking the next item when free
-            bool busy = false;
-            uint32_t item = 0u, phit = 0u;
-            float pclose = 0.0f;
-            Ray pr{};
-            V pinv = mk(0.0f, 0.0f, 0.0f);
-            Trav ptv{};
-            uint32_t* pstk = stk;
-            for (;;) {
-                const unsigned long long idle = __ballot(!busy);
-                uint32_t t0 = 0u;
-                if (idle) {
-                    if (lane == 0u) t0 = atomicAdd(&ctr[1], (uint32_t)__popcll(idle));
-                    t0 = __builtin_amdgcn_readfirstlane(t0);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // the items before their ready bits
+#ifdef RT_POOL_CHECK
+    if (lane == 0u) {
+        if (atomicOr(&ready[wave], own) & own) pool_anomaly(8, wave);  // stale ready bits
+        if (__hip_atomic_load(&done[wave], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & own)
+            pool_anomaly(9, wave);  // stale done bits
+    }
+#else
+    if (lane == 0u) atomicOr(&ready[wave], own);
+#endif
+    // phase 2: serve the pool while this wave holds the token, else wait for the own items
+    bool server = false, busy = false;
+    uint32_t item = 0u, phit = 0u, proot = 0u;
+    float pclose = 0.0f;
+    Ray pr{};
+    V pinv = mk(0.0f, 0.0f, 0.0f);
+    Trav ptv{};
+    uint32_t* pstk = stk;
+    for (;;) {
+        // the ready slots of all waves as one mask (bit w * kPoolPost + b)
+        auto ready_all = [&]() {
+            unsigned long long m = 0ull;
+            for (uint32_t w = 0; w < kPoolWaves; ++w)
+                m |= (unsigned long long)__hip_atomic_load(&ready[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
+                     << (w * kPoolPost);
+            // (readfirstlane returns int: widen through uint32_t, a sign-extended low word
+            // would show every slot of waves 2-3 ready whenever slot 31 is)
+            return (unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)m) |
+                   ((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(m >> 32)) << 32);
+        };
+        if (!server) {  // take the token when it is free and work is ready
+            uint32_t got = 0u;
+            if (ready_all() != 0ull && lane == 0u) {
+                uint32_t expect = 0u;
+                got = __hip_atomic_compare_exchange_strong(token, &expect, wave + 1u, __ATOMIC_ACQUIRE, __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_WORKGROUP)
+                          ? 1u
+                          : 0u;
+            }
+            server = __builtin_amdgcn_readfirstlane(got) != 0u;
+            // the previous server's clears happened before its release of the token: no ready
+            // snapshot from before the acquisition may be reused (it may hold items served since)
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        }
+        unsigned long long left = 0ull;  // items still ready after this refill
+        if (server) {  // refill the idle lanes with ready items (only the server clears ready bits)
+            const unsigned long long idle = __ballot(!busy);
+            unsigned long long take = 0ull;
+            if (idle) {
+                unsigned long long m = ready_all();
+                for (uint32_t k = (uint32_t)__popcll(idle); k != 0u && m != 0ull; --k) {
+                    const unsigned long long bit = m & (0ull - m);
+                    take |= bit;
+                    m &= m - 1ull;
                 }
-                if (!busy) {
-                    const uint32_t it =
-                        t0 + __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
-                    if (it < n) {
+                left = m;
+                if (take) {
+                    if (lane < kPoolWaves) {
+                        const uint32_t tw = (uint32_t)(take >> (lane * kPoolPost)) & ((1u << kPoolPost) - 1u);
+#ifdef RT_POOL_CHECK
+                        if (tw && (atomicAnd(&ready[lane], ~tw) & tw) != tw) pool_anomaly(10, wave);
+                        if (tw && (__hip_atomic_load(&done[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & tw))
+                            pool_anomaly(11, wave);
+#else
+                        if (tw) atomicAnd(&ready[lane], ~tw);
+#endif
+                    }
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                    // the r-th idle lane takes the r-th taken slot
+                    const uint32_t ir = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
+                                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
+                    uint32_t it = kPoolCap;
+                    unsigned long long t = take;
+                    for (uint32_t j = 0; t != 0ull; ++j) {
+                        const uint32_t bpos = (uint32_t)__builtin_ctzll(t);
+                        t &= t - 1ull;
+                        if (!busy && ir == j) it = bpos;
+                    }
+                    if (!busy && it < kPoolCap) {
                         const uint32_t* q = P + it;
                         pr.o = mk(__uint_as_float(q[0 * kPoolCap]), __uint_as_float(q[1 * kPoolCap]),
                                   __uint_as_float(q[2 * kPoolCap]));
@@ -1991,41 +2067,86 @@ RT_DEV void bvh_pool(const DevScene& S, float delta, const DevEntry* E, const Ra
                                    (br >> 31) != 0u, q[16 * kPoolCap]};
                         // the owner's stack column: wave (sid >> 6) & 3 of this workgroup, lane sid & 63
                         pstk = lds + ((ptv.sid >> 6) & (kPoolWaves - 1u)) * region + (ptv.sid & 63u);
+                        proot = q[17 * kPoolCap];
                         item = it;
                         busy = true;
-                    }
-                }
-                if (__ballot(busy) == 0ull) break;
-                const bool more = t0 + (uint32_t)__popcll(idle) < n;  // items still in the pool
-                if (busy) {
-                    if (bvh_run<0, kF, true>(S, delta, wrapper, pr, pinv, 0.001f, pclose, phit, pstk, mode, ptv,
-                                             more ? kPoolRefill : 0u)) {
-                        trav_audit(S, wrapper, root, pr, pinv, 0.001f, ptv, pclose, phit, pstk);
-                        uint32_t* q = P + item;
-                        q[11 * kPoolCap] = __float_as_uint(pclose);
-                        q[12 * kPoolCap] = phit;
-                        q[13 * kPoolCap] = ptv.best_rank | (ptv.any ? 0x80000000u : 0u);
-                        busy = false;
+#ifdef RT_POOL_CHECK
+                        atomicAdd(&g_pool_check[3], 1u);
+                        if (((ptv.sid >> 6) & 3u) != wave) atomicAdd(&g_pool_check[4], 1u);
+                        const bool bad_cur = (ptv.cur & ~rtdev::kLeafNodeFlag) >= S.num_nodes;
+                        const bool bad_sp = ptv.sp > S.stack_depth + S.spill_depth;
+                        const bool bad_sid = (ptv.sid >> 8) != blockIdx.x || it / kPoolPost != ((ptv.sid >> 6) & 3u);
+                        if (bad_cur) atomicAdd(&g_pool_check[5], 1u);
+                        if (bad_sp) atomicAdd(&g_pool_check[6], 1u);
+                        if (bad_sid) atomicAdd(&g_pool_check[7], 1u);
+                        if (bad_cur || bad_sp || bad_sid) {
+                            atomicCAS(&g_pool_first, 0u, (12u << 24) | (blockIdx.x << 2) | wave);
+                            if (atomicAdd(&g_pool_check[0], 1u) == 0u) {
+                                for (uint32_t w = 0; w < 17u; ++w) g_pool_dump[w] = (P + it)[w * kPoolCap];
+                                g_pool_dump[17] = it;
+                                g_pool_dump[18] = blockIdx.x;
+                                g_pool_dump[19] = wave;
+                                g_pool_dump[20] = ready[0];
+                                g_pool_dump[21] = ready[1];
+                                g_pool_dump[22] = ready[2];
+                                g_pool_dump[23] = ready[3];
+                            }
+                            uint32_t* q2 = P + it;
+                            q2[11 * kPoolCap] = __float_as_uint(ptv.tmax_entry);
+                            q2[12 * kPoolCap] = 0u;
+                            q2[13 * kPoolCap] = 0u;
+                            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                            atomicOr(&done[it / kPoolPost], 1u << (it % kPoolPost));
+                            busy = false;
+                        }
+#endif
                     }
                 }
             }
         }
+        if (__ballot(busy) != 0ull) {
+            if (busy) {
+                const f4* pwrap = S.nodes + (size_t)proot * rtdev::kBvhNodeF4;
+                if (bvh_run<0, kF, true>(S, delta, pwrap, pr, pinv, 0.001f, pclose, phit, pstk, mode, ptv,
+                                         left ? kPoolRefill : 0u)) {
+                    trav_audit(S, pwrap, proot, pr, pinv, 0.001f, ptv, pclose, phit, pstk);
+                    uint32_t* q = P + item;
+                    q[11 * kPoolCap] = __float_as_uint(pclose);
+                    q[12 * kPoolCap] = phit;
+                    q[13 * kPoolCap] = ptv.best_rank | (ptv.any ? 0x80000000u : 0u);
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // the result before its done bit
+                    atomicOr(&done[item / kPoolPost], 1u << (item % kPoolPost));
+                    busy = false;
+                }
+            }
+            continue;
+        }
+        // no lane busy: hand the token back when nothing is ready, leave once the own items are done
+        const uint32_t d = __builtin_amdgcn_readfirstlane(
+            __hip_atomic_load(&done[wave], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+        const bool mine_done = (d & own) == own;
+        if (server && ready_all() == 0ull) {
+            if (lane == 0u) __hip_atomic_store(token, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            server = false;
+        }
+        if (mine_done && !server) break;
+        if (!server) __builtin_amdgcn_s_sleep(2);
     }
-    __syncthreads();
-    if (post) {  // phase 3: the owner takes its traversal's result
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    if (post) {  // the owner takes its traversal's result
         const uint32_t* q = P + slot;
         closest = __uint_as_float(q[11 * kPoolCap]);
         hit_code = q[12 * kPoolCap];
         any_out = (q[13 * kPoolCap] >> 31) != 0u;
+#ifdef RT_POOL_CHECK
+        if (q[16 * kPoolCap] != self_sid()) atomicAdd(&g_pool_check[1], 1u);
+        if (any_out && (!(hit_code & rtdev::kLeafBit) || rtdev::leaf_index(hit_code) > 0x00ffffffu)) {
+            atomicAdd(&g_pool_check[2], 1u);
+            any_out = false;
+        }
+#endif
     }
-    // the first claimer (alive: it just passed both barriers) clears this pool's counters for
-    // their next use two calls on; every read of them happened before the second barrier, and the
-    // next post into this pool follows the next call's first barrier
-    if (claim == 0u && lane == 0u) {
-        ctr[0] = 0u;
-        ctr[1] = 0u;
-        ctr[2] = 0u;
-    }
+    if (lane == 0u) atomicAnd(&done[wave], ~own);
 }
 
 // HittableList::hit over the world (hittable.rs:100-118) for kFPool instances: world_hit, with
@@ -2035,7 +2156,7 @@ RT_DEV void bvh_pool(const DevScene& S, float delta, const DevEntry* E, const Ra
 template <uint32_t kF>
 RT_DEV bool world_hit_pool(const DevScene& S, float delta, const Ray& r, bool active, Rng& g, const Key& k,
                            float& t_hit, uint32_t& hit_entry, uint32_t& hit_code, uint32_t* lds, uint32_t* stk,
-                           uint32_t lane, uint32_t& call, uint32_t mode, bool& replay) {
+                           uint32_t wave, uint32_t lane, uint32_t mode, bool& replay) {
     float closest = kInf;
     bool any = false;
     for (uint32_t e = 0; e < S.num_top; ++e) {
@@ -2043,7 +2164,7 @@ RT_DEV bool world_hit_pool(const DevScene& S, float delta, const Ray& r, bool ac
         if (E->kind == rtdev::kEntBvh) {
             bool h = false;
             uint32_t code = hit_code;
-            bvh_pool<kF>(S, delta, E, r, active, closest, code, h, lds, stk, lane, call, mode, replay);
+            bvh_pool<kF>(S, delta, E, r, active, closest, code, h, lds, stk, wave, lane, mode, replay);
             if (h) {
                 hit_entry = e;
                 hit_code = code;
@@ -2485,10 +2606,9 @@ __global__ __launch_bounds__((kF & kFPool) != 0u ? 64u * kPoolWaves : 64u, kWave
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     DevScene S = Sg;
     uint32_t* stk = lds_stack + wave * S.stack_depth * 128u + lane;  // [level][{node, t_enter}][lane]
-    [[maybe_unused]] uint32_t pool_call = 0u;  // kFPool: top-level BVH calls so far (the same in every wave)
-    [[maybe_unused]] uint32_t pool_trip = 0u;  // kFPool: sample-loop trips so far (the same in every wave)
-    if constexpr ((kF & kFPool) != 0u) {
-        if (threadIdx.x < 16u) lds_stack[kPoolWaves * S.stack_depth * 128u + 2u * kPoolWords * kPoolCap + threadIdx.x] = 0u;
+    if constexpr ((kF & kFPool) != 0u) {  // the pool's masks and token start clear
+        if (threadIdx.x < 2u * kPoolWaves + 1u)
+            lds_stack[kPoolWaves * S.stack_depth * 128u + kPoolWords * kPoolCap + threadIdx.x] = 0u;
         __syncthreads();
     }
     // Perlin permutation tables (Marble) behind the stack when they fit: the
@@ -2603,9 +2723,7 @@ __global__ __launch_bounds__((kF & kFPool) != 0u ? 64u * kPoolWaves : 64u, kWave
             has = true;
         }
         PROF_ADD(kPrRefill, pr);
-        if constexpr ((kF & kFPool) != 0u) {  // the workgroup's waves end together (pool_live)
-            if (!pool_live(lds_stack, S.stack_depth * 128u, __ballot(has) != 0ull, wave, lane, pool_trip)) break;
-        } else if (__ballot(has) == 0ull) {
+        if (__ballot(has) == 0ull) {
             break;  // pool exhausted and every path finished
         }
 #ifdef RT_PROFILE_REGIONS
@@ -2624,8 +2742,8 @@ __global__ __launch_bounds__((kF & kFPool) != 0u ? 64u * kPoolWaves : 64u, kWave
             float t = 0.0f;
             uint32_t he = 0, hc = 0;
             PROF_T0(pw);
-            any = world_hit_pool<kF>(S, P.prune_delta, ray, has, g, k, t, he, hc, lds_stack, stk, lane, pool_call,
-                                     mode, replay);
+            any = world_hit_pool<kF>(S, P.prune_delta, ray, has, g, k, t, he, hc, lds_stack, stk, wave, lane, mode,
+                                     replay);
             PROF_ADD(kPrWorld, pw);
             bool shade = has;
             if (has && replay) {  // hand the sample to the reference kernel
@@ -3104,9 +3222,8 @@ int rt_scene_upload(const rt_scene_desc* desc, int device, rt_scene_handle* out)
         if (e.kind == rtdev::kEntBvh) s->features |= kFBvh;
         if (e.kind == rtdev::kEntSphereRun && e.pad[0] >= kRunPretestMin) s->features |= kFRuns;
     }
-    // the sphere-BVH + Marble preset (showcase) traverses through the workgroup pool (kFPool)
-    // unless RT_OPT_TUNE's kModeNoPool (A/B, tests) says otherwise
-    const bool pool = s->features == (kFBvh | kFMarble) && !(opt(RT_OPT_TUNE) & kModeNoPool);
+    // RT_OPT_TUNE's kModePool (A/B, tests): the sphere-BVH + Marble preset through the workgroup pool
+    const bool pool = s->features == (kFBvh | kFMarble) && (opt(RT_OPT_TUNE) & kModePool);
     if (pool) s->features |= kFPool;
 #ifndef RT_LEAF_AUDIT  // (the audit build replays traversals on the same LDS stack: no spill area)
     {  // deep BVHs: the LDS stack keeps kStackLdsMax entries (kPoolStackLds in pool instances), HBM the rest
@@ -3223,6 +3340,25 @@ int rt_scene_free(rt_scene_handle s) {
         }
         if (hipMemcpyFromSymbol(&na, HIP_SYMBOL(g_bounds_audit_count), sizeof na) == hipSuccess)
             fprintf(stderr, "{\"bounds_audit_count\": %u}\n", na);
+#endif
+#ifdef RT_POOL_CHECK
+        {
+            unsigned first = 0;
+            if (hipMemcpyFromSymbol(&first, HIP_SYMBOL(g_pool_first), sizeof first) == hipSuccess)
+                fprintf(stderr, "{\"pool_first\": [%u, %u, %u]}\n", first >> 24, (first & 0xffffffu) >> 2, first & 3u);
+            unsigned pc[16] = {};
+            if (hipDeviceSynchronize() == hipSuccess && hipMemcpyFromSymbol(pc, HIP_SYMBOL(g_pool_check), sizeof pc) == hipSuccess) {
+                fprintf(stderr, "{\"pool_check\": [");
+                for (int i = 0; i < 16; ++i) fprintf(stderr, "%s%u", i ? ", " : "", pc[i]);
+                fprintf(stderr, "]}\n");
+            }
+            unsigned dump[24] = {};
+            if (hipMemcpyFromSymbol(dump, HIP_SYMBOL(g_pool_dump), sizeof dump) == hipSuccess) {
+                fprintf(stderr, "{\"pool_dump\": [");
+                for (int i = 0; i < 24; ++i) fprintf(stderr, "%s%u", i ? ", " : "", dump[i]);
+                fprintf(stderr, "]}\n");
+            }
+        }
 #endif
         if (s->done) (void)hipEventSynchronize(s->done);  // the last launch may still use the buffers below
         if (s->pool) (void)hipFree(s->pool);
