@@ -984,14 +984,13 @@ RT_DEV void sort2(float& ta, uint32_t& ca, float& tb, uint32_t& cb) {  // branch
 // to an axis plane (a zero direction component) gets t = (k - o) / d = 0 / 0 from
 // a rect whose plane holds its origin, and every comparison against NaN passes
 // (rectangle.rs:36-65); its sample is re-traced by the reference kernel.
-// A BVH traversal's state between visits (bvh_run). sid: the global thread id (wave * 64 + lane)
-// of the lane that owns the traversal's stack (its LDS column and, for deep stacks, its HBM spill
-// slab): the lane itself, or another wave's lane whose traversal it took over (kFPool).
+// A BVH traversal's state between visits (bvh_run). A kFPool traversal's stack owner (its LDS
+// column and, for deep stacks, its HBM spill slab) travels beside it as a sid: the global thread
+// id (wave * 64 + lane) of the lane that started it, which may be another wave's lane.
 struct Trav {
     uint32_t cur, sp, best_rank;
     float tmax_entry;
     bool any;
-    uint32_t sid;
 };
 RT_DEV uint32_t self_sid() { return blockIdx.x * blockDim.x + threadIdx.x; }
 // Audit build: every completed fast traversal is replayed with the reference recursion
@@ -1025,7 +1024,7 @@ RT_DEV void trav_audit(const DevScene& S, const f4* wrapper, uint32_t root, cons
 constexpr uint32_t kSuspMinTrips = RT_SUSP_MIN_TRIPS;
 template <int kKind, uint32_t kF, bool kSusp>
 RT_DEV bool bvh_run(const DevScene& S, float delta, const f4* wrapper, const Ray& r, V inv, float tmin, float& closest,
-                    uint32_t& hit_code, uint32_t* stk, uint32_t mode, Trav& tv, uint32_t susp);
+                    uint32_t& hit_code, uint32_t* stk, uint32_t mode, Trav& tv, uint32_t susp, uint32_t sid = 0u);
 template <int kKind, uint32_t kF = kFAll>
 RT_DEV bool bvh_hit(const DevScene& S, float delta, uint32_t root, const Ray& r, float tmin, float& closest,
                     uint32_t& hit_code, uint32_t* stk, uint32_t mode, bool& replay) {
@@ -1066,7 +1065,7 @@ RT_DEV bool bvh_hit(const DevScene& S, float delta, uint32_t root, const Ray& r,
         }
     }
     PROF_ADD(kPrBvhSetup, psetup);
-    Trav tv{root, 0u, 0u, closest, false, self_sid()};
+    Trav tv{root, 0u, 0u, closest, false};
     bvh_run<kKind, kF, false>(S, delta, wrapper, r, inv, tmin, closest, hit_code, stk, mode, tv, 0u);
     const bool any = tv.any;
     PROF_ADD(kPrBvhCall, pcall);
@@ -1086,7 +1085,7 @@ RT_DEV bool bvh_hit(const DevScene& S, float delta, uint32_t root, const Ray& r,
 // visit runs differs, so the result is the same bits.
 template <int kKind, uint32_t kF, bool kSusp>
 RT_DEV bool bvh_run(const DevScene& S, float delta, const f4* wrapper, const Ray& r, V inv, float tmin, float& closest,
-                    uint32_t& hit_code, uint32_t* stk, uint32_t mode, Trav& tv, uint32_t susp) {
+                    uint32_t& hit_code, uint32_t* stk, uint32_t mode, Trav& tv, uint32_t susp, uint32_t sid) {
     const float tmax_entry = tv.tmax_entry;
     const bool prune = (__float_as_uint(wrapper[7].w) & rtdev::kBvhPrunable) != 0u || (mode & kModePruneAllExp);
     const float dmi = delta * fmaxf(fmaxf(__builtin_fabsf(inv.x), __builtin_fabsf(inv.y)), __builtin_fabsf(inv.z));
@@ -1097,7 +1096,15 @@ RT_DEV bool bvh_run(const DevScene& S, float delta, const f4* wrapper, const Ray
                                     hnz = inv.z < 0.0f ? 80u : 32u;
     bool any = tv.any;
     uint32_t best_rank = tv.best_rank, sp = tv.sp, cur = tv.cur;
-    [[maybe_unused]] const uint32_t sid = tv.sid;
+    // kFDeep: stack entry sp of this traversal in its owner wave's HBM slab. One-wave workgroups
+    // address it from the scalar block index (a per-lane sid costs C4 9%); a pool instance's
+    // traversal may run in another wave's lane, so it carries its owner in Trav::sid.
+    [[maybe_unused]] auto slab = [&](uint32_t spi) -> uint32_t* {
+        if constexpr ((kF & kFPool) != 0u)
+            return S.stack_spill + (((size_t)(sid >> 6) * S.spill_depth + (spi - S.stack_depth)) * 64u + (sid & 63u)) * 2u;
+        else  // (a wave-uniform base and a 32-bit lane offset: the load takes the scalar-base form)
+            return S.stack_spill + (size_t)blockIdx.x * S.spill_depth * 128u + ((spi - S.stack_depth) * 64u + threadIdx.x) * 2u;
+    };
     bool finished = true;
     [[maybe_unused]] uint32_t trips = 0;
 #ifdef RT_PROFILE_REGIONS
@@ -1259,8 +1266,7 @@ RT_DEV bool bvh_run(const DevScene& S, float delta, const f4* wrapper, const Ray
                 stk[sp * 128u] = node;
                 stk[sp * 128u + 64u] = __float_as_uint(t);
             } else {
-                uint32_t* g = S.stack_spill +
-                              (((size_t)(sid >> 6) * S.spill_depth + (sp - S.stack_depth)) * 64u + (sid & 63u)) * 2u;
+                uint32_t* g = slab(sp);
                 g[0] = node;
                 g[1] = __float_as_uint(t);
             }
@@ -1285,8 +1291,7 @@ RT_DEV bool bvh_run(const DevScene& S, float delta, const f4* wrapper, const Ray
                 cand = stk[sp * 128u];
                 tenter = __uint_as_float(stk[sp * 128u + 64u]);
             } else {
-                const uint32_t* g = S.stack_spill +
-                                    (((size_t)(sid >> 6) * S.spill_depth + (sp - S.stack_depth)) * 64u + (sid & 63u)) * 2u;
+                const uint32_t* g = slab(sp);
                 cand = g[0];
                 tenter = __uint_as_float(g[1]);
             }
@@ -1299,7 +1304,7 @@ RT_DEV bool bvh_run(const DevScene& S, float delta, const f4* wrapper, const Ray
         PROF_ADD(kPrBvhPop, ppop);
         if (!found) break;
     }
-    tv = Trav{cur, sp, best_rank, tmax_entry, any, sid};
+    tv = Trav{cur, sp, best_rank, tmax_entry, any};
 #ifdef RT_PROFILE_REGIONS
     {
         const uint32_t b = trips_bin(visits);
@@ -1930,10 +1935,11 @@ RT_DEV void bvh_pool(const DevScene& S, float delta, const DevEntry* E, const Ra
         if (!fast) replay = true;
         mine = fast;
     }
-    Trav tv{root, 0u, 0u, closest, false, self_sid()};
+    Trav tv{root, 0u, 0u, closest, false};
     bool post = false;
     if (mine) {  // phase 1: the wave's own traversals, until at most kPoolPost lanes still traverse
-        if (bvh_run<0, kF, true>(S, delta, wrapper, r, inv, 0.001f, closest, hit_code, stk, mode, tv, kPoolPost)) {
+        if (bvh_run<0, kF, true>(S, delta, wrapper, r, inv, 0.001f, closest, hit_code, stk, mode, tv, kPoolPost,
+                                 self_sid())) {
             trav_audit(S, wrapper, root, r, inv, 0.001f, tv, closest, hit_code, stk);
             any_out = tv.any;
         } else {
@@ -1970,7 +1976,7 @@ RT_DEV void bvh_pool(const DevScene& S, float delta, const DevEntry* E, const Ra
         q[13 * kPoolCap] = tv.best_rank | (tv.any ? 0x80000000u : 0u);
         q[14 * kPoolCap] = tv.cur;
         q[15 * kPoolCap] = tv.sp;
-        q[16 * kPoolCap] = tv.sid;
+        q[16 * kPoolCap] = self_sid();
         q[17 * kPoolCap] = root;  // waves run asynchronously: the server may be at another entry
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // the items before their ready bits
@@ -1985,7 +1991,7 @@ RT_DEV void bvh_pool(const DevScene& S, float delta, const DevEntry* E, const Ra
 #endif
     // phase 2: serve the pool while this wave holds the token, else wait for the own items
     bool server = false, busy = false;
-    uint32_t item = 0u, phit = 0u, proot = 0u;
+    uint32_t item = 0u, phit = 0u, proot = 0u, psid = 0u;
     float pclose = 0.0f;
     Ray pr{};
     V pinv = mk(0.0f, 0.0f, 0.0f);
@@ -2064,18 +2070,19 @@ RT_DEV void bvh_pool(const DevScene& S, float delta, const DevEntry* E, const Ra
                         phit = q[12 * kPoolCap];
                         const uint32_t br = q[13 * kPoolCap];
                         ptv = Trav{q[14 * kPoolCap], q[15 * kPoolCap], br & 0x7fffffffu, __uint_as_float(q[10 * kPoolCap]),
-                                   (br >> 31) != 0u, q[16 * kPoolCap]};
+                                   (br >> 31) != 0u};
+                        psid = q[16 * kPoolCap];
                         // the owner's stack column: wave (sid >> 6) & 3 of this workgroup, lane sid & 63
-                        pstk = lds + ((ptv.sid >> 6) & (kPoolWaves - 1u)) * region + (ptv.sid & 63u);
+                        pstk = lds + ((psid >> 6) & (kPoolWaves - 1u)) * region + (psid & 63u);
                         proot = q[17 * kPoolCap];
                         item = it;
                         busy = true;
 #ifdef RT_POOL_CHECK
                         atomicAdd(&g_pool_check[3], 1u);
-                        if (((ptv.sid >> 6) & 3u) != wave) atomicAdd(&g_pool_check[4], 1u);
+                        if (((psid >> 6) & 3u) != wave) atomicAdd(&g_pool_check[4], 1u);
                         const bool bad_cur = (ptv.cur & ~rtdev::kLeafNodeFlag) >= S.num_nodes;
                         const bool bad_sp = ptv.sp > S.stack_depth + S.spill_depth;
-                        const bool bad_sid = (ptv.sid >> 8) != blockIdx.x || it / kPoolPost != ((ptv.sid >> 6) & 3u);
+                        const bool bad_sid = (psid >> 8) != blockIdx.x || it / kPoolPost != ((psid >> 6) & 3u);
                         if (bad_cur) atomicAdd(&g_pool_check[5], 1u);
                         if (bad_sp) atomicAdd(&g_pool_check[6], 1u);
                         if (bad_sid) atomicAdd(&g_pool_check[7], 1u);
@@ -2108,7 +2115,7 @@ RT_DEV void bvh_pool(const DevScene& S, float delta, const DevEntry* E, const Ra
             if (busy) {
                 const f4* pwrap = S.nodes + (size_t)proot * rtdev::kBvhNodeF4;
                 if (bvh_run<0, kF, true>(S, delta, pwrap, pr, pinv, 0.001f, pclose, phit, pstk, mode, ptv,
-                                         left ? kPoolRefill : 0u)) {
+                                         left ? kPoolRefill : 0u, psid)) {
                     trav_audit(S, pwrap, proot, pr, pinv, 0.001f, ptv, pclose, phit, pstk);
                     uint32_t* q = P + item;
                     q[11 * kPoolCap] = __float_as_uint(pclose);
@@ -2242,7 +2249,7 @@ RT_DEV void world_walk(const DevScene& S, float delta, const Ray& ray, Rng& g, c
                     w.pos = S.num_top + 1u;  // abandoned: the sample is re-traced by the reference kernel
                     continue;
                 }
-                w.tv = Trav{root, 0u, 0u, w.closest, false, self_sid()};
+                w.tv = Trav{root, 0u, 0u, w.closest, false};
             }
             if (bvh_run<0, kF, true>(S, delta, wrapper, r, inv, 0.001f, w.closest, w.hit_code, stk, mode, w.tv, susp)) {
                 trav_audit(S, wrapper, root, r, inv, 0.001f, w.tv, w.closest, w.hit_code, stk);
@@ -2352,9 +2359,9 @@ RT_DEV bool take_sample(ItemPool& pool, bool want, const DevCamera& C, const Dev
                         const Key& k, unsigned* counter, const ReplayItem* list, uint32_t list_n,
                         TraceCounters* ctr, uint32_t stream_grid, float* sbuf,
                         uint32_t lane, uint32_t& slot, uint32_t& s_local, V& L, V& T, uint32_t& depth, Rng& g,
-                        Ray& ray) {
+                        Ray& ray, uint32_t wg_waves) {
     bool got = false;
-    const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);  // waves of the launch
+    const uint32_t nwaves = gridDim.x * wg_waves;  // waves of the launch (wg_waves: a compile-time 1 or kPoolWaves)
     for (;;) {
         unsigned long long need = __ballot(want && !got);
         if (need == 0ull || pool.exhausted) break;
@@ -2602,8 +2609,10 @@ __global__ __launch_bounds__((kF & kFPool) != 0u ? 64u * kPoolWaves : 64u, kWave
     extern __shared__ uint32_t lds_stack[];
     // kFPool instances run kPoolWaves waves per workgroup (one stack region per wave, then the
     // pool); every other instance one wave per workgroup
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // (one-wave instances keep the plain thread index: the pool's wave split costs them registers)
+    constexpr uint32_t wg_waves = (kF & kFPool) != 0u ? kPoolWaves : 1u;
+    const uint32_t lane = wg_waves > 1u ? threadIdx.x & 63u : threadIdx.x;
+    const uint32_t wave = wg_waves > 1u ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : 0u;
     DevScene S = Sg;
     uint32_t* stk = lds_stack + wave * S.stack_depth * 128u + lane;  // [level][{node, t_enter}][lane]
     if constexpr ((kF & kFPool) != 0u) {  // the pool's masks and token start clear
@@ -2681,7 +2690,7 @@ __global__ __launch_bounds__((kF & kFPool) != 0u ? 64u * kPoolWaves : 64u, kWave
         for (;;) {
             PROF_T0(pr);
             if (take_sample(pool, !has, C, P, Q, k, counter, list, list_n, ctr, stream_grid, sbuf, lane, slot, take_sample_idx, L, T, depth, g,
-                            ray)) {
+                            ray, wg_waves)) {
                 has = true;
                 w.pos = 0u;
                 w.resume = false;
@@ -2719,7 +2728,7 @@ __global__ __launch_bounds__((kF & kFPool) != 0u ? 64u * kPoolWaves : 64u, kWave
     for (;;) {
         PROF_T0(pr);
         if (take_sample(pool, !has, C, P, Q, k, counter, list, list_n, ctr, stream_grid, sbuf, lane, slot, take_sample_idx, L, T, depth, g,
-                        ray)) {
+                        ray, wg_waves)) {
             has = true;
         }
         PROF_ADD(kPrRefill, pr);
