@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--rank", type=int, default=0)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--spp", type=int, default=None, help="override the config's samples per pixel")
+    ap.add_argument("--shard-only", action="store_true", help="skip the whole-frame (1-rank) reference run")
     a = ap.parse_args()
     import torch
     import raytracinginoneweekendinrust_amd as rt
@@ -32,7 +33,7 @@ def main():
     scene = rt.Scene.generate(cfg.scene, cfg.scene_seed)
     ds = rt.DeviceScene(scene)
     out = torch.zeros(cfg.width * cfg.height * 3, dtype=torch.float32, device="cuda")
-    for n in sorted({1, a.n}):
+    for n in ([a.n] if a.shard_only else sorted({1, a.n})):
         p = rt.render_params(cfg.width, cfg.height, cfg.spp, cfg.depth, background=cfg.background(),
                              seed=cfg.render_seed, shard_index=a.rank if n > 1 else 0, shard_count=n)
         ds.launch(cfg.camera(), p, out.data_ptr(), 0, 0)  # warm-up
