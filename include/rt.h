@@ -200,6 +200,30 @@ typedef struct rt_tile {
     uint32_t width, height, x_start, y_start;
 } rt_tile;
 
+/* The layouts a foreign binding mirrors byte for byte (INTEGRATION.md's #[repr(C)] structs,
+ * the ctypes mirror in raytracinginoneweekendinrust_amd/_capi.py): every C or C++ compile of
+ * this header checks them. */
+#ifdef __cplusplus
+#define RT_LAYOUT_ASSERT(cond, what) static_assert(cond, what)
+#else
+#define RT_LAYOUT_ASSERT(cond, what) _Static_assert(cond, what)
+#endif
+RT_LAYOUT_ASSERT(sizeof(rt_node) == 72 && offsetof(rt_node, ref) == 4 && offsetof(rt_node, f) == 16 &&
+                     offsetof(rt_node, seed) == 64, "rt_node layout");
+RT_LAYOUT_ASSERT(sizeof(rt_bvh_node) == 40 && offsetof(rt_bvh_node, bbox_min) == 16 &&
+                     offsetof(rt_bvh_node, bbox_max) == 28, "rt_bvh_node layout");
+RT_LAYOUT_ASSERT(sizeof(rt_scene_desc) == 64 && offsetof(rt_scene_desc, list_items) == 16 &&
+                     offsetof(rt_scene_desc, image_data) == 32 && offsetof(rt_scene_desc, image_bytes) == 40 &&
+                     offsetof(rt_scene_desc, bvh_nodes) == 48 && offsetof(rt_scene_desc, num_bvh_nodes) == 56,
+                 "rt_scene_desc layout");
+RT_LAYOUT_ASSERT(sizeof(rt_camera) == 84 && offsetof(rt_camera, lens_radius) == 72 &&
+                     offsetof(rt_camera, time_end) == 80, "rt_camera layout");
+RT_LAYOUT_ASSERT(sizeof(rt_render_params) == 64 && offsetof(rt_render_params, seed) == 24 &&
+                     offsetof(rt_render_params, sample_base) == 32 && offsetof(rt_render_params, flags) == 44 &&
+                     offsetof(rt_render_params, background) == 48 && offsetof(rt_render_params, spp_total) == 60,
+                 "rt_render_params layout");
+RT_LAYOUT_ASSERT(sizeof(rt_stats) == 24 && offsetof(rt_stats, kernel_ms) == 16, "rt_stats layout");
+
 typedef struct rt_scene* rt_scene_handle;
 
 /* ------------------------------------------------------------------------ */

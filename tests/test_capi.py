@@ -160,3 +160,25 @@ def test_diagnostic_options_are_explicit(rt):
         with pytest.raises(rt.RTError, match="RT_ERR_INVALID"):
             rt.set_option(name, bad)
     assert _capi.lib.rt_set_option(99, 0) == -1
+
+
+def test_abi_layouts_match_the_header_and_the_ctypes_mirror(tmp_path):
+    # include/rt.h asserts its struct layouts (RT_LAYOUT_ASSERT) on every C / C++ compile; the
+    # ctypes mirror and INTEGRATION.md's #[repr(C)] structs must describe the same bytes.
+    from raytracinginoneweekendinrust_amd import _capi
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    inc = os.path.join(root, "include")
+    src = tmp_path / "layout.c"
+    src.write_text('#include "rt.h"\nint main(void) { return 0; }\n')
+    for compiler, std in (("gcc", "-std=c11"), ("g++", "-std=c++17")):
+        r = subprocess.run([compiler, std, "-fsyntax-only", "-I", inc, "-x", "c" if compiler == "gcc" else "c++",
+                            str(src)], capture_output=True, text=True)
+        assert r.returncode == 0, r.stderr
+    sizes = {"rt_node": 72, "rt_bvh_node": 40, "rt_scene_desc": 64, "rt_camera": 84, "rt_render_params": 64,
+             "rt_stats": 24}
+    for name, size in sizes.items():
+        assert C.sizeof(getattr(_capi, name)) == size, name
+    assert _capi.rt_render_params.seed.offset == 24 and _capi.rt_render_params.spp_total.offset == 60
+    assert _capi.rt_scene_desc.bvh_nodes.offset == 48 and _capi.rt_node.seed.offset == 64
+    doc = open(os.path.join(root, "INTEGRATION.md")).read()
+    assert "rt_node = 72 B, rt_bvh_node = 40 B, rt_scene_desc = 64 B, rt_camera = 84 B, rt_render_params = 64 B" in doc
