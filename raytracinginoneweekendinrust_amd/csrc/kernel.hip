@@ -80,10 +80,6 @@ constexpr uint32_t kModePruneAllExp = 1u << 20;
 // 8: C3 69.7 -> 68.0 ms, C1 -3%). BlocksForward (RT_OPT_TUNE, A/B only) restores
 // the top-first order. Either order gives the same bits (samples are keyed by pixel and index).
 constexpr uint32_t kModeBlocksForward = 1u << 21;
-// Pool (RT_OPT_TUNE at rt_scene_upload; A/B and tests): the sphere-BVH + Marble preset through the
-// cross-wave traversal pool (kFPool) instead of the one-wave instance. Bit-exact, and slower: C3 at
-// 100 spp 102 ms without, 192-209 ms with it (profiles/r03/pool/), so it is not the default.
-constexpr uint32_t kModePool = 1u << 22;
 #ifdef RT_ABLATE
 // Ablation build (librtamd_ablate.so, diagnostics only): RT_OPT_TUNE bits that run a
 // piece of work twice (results of the copy discarded through an opaque test),
@@ -135,10 +131,10 @@ __device__ __forceinline__ void prof_flush() {
 __device__ __forceinline__ void prof_add(uint32_t region, uint64_t t0) {
     uint64_t dt = __builtin_amdgcn_s_memtime() - t0;
     uint64_t m = __ballot(1);
-    if (__lane_id() == (uint32_t)__builtin_ctzll(m)) {  // atomics: a kFPool workgroup's waves share prof_lds
-        atomicAdd(&prof_lds[region], (unsigned long long)dt);
-        atomicAdd(&prof_lds[kPrCount + region], 1ull);
-        atomicAdd(&prof_lds[2 * kPrCount + region], (unsigned long long)__popcll(m));
+    if (__lane_id() == (uint32_t)__builtin_ctzll(m)) {
+        prof_lds[region] += dt;
+        prof_lds[kPrCount + region] += 1u;
+        prof_lds[2 * kPrCount + region] += (uint64_t)__popcll(m);
     }
 }
 #define PROF_INIT() prof_init()
@@ -173,25 +169,6 @@ __device__ unsigned g_bounds_audit_count;
 __device__ TravAudit g_trav_audit[kAuditMax];
 #endif
 
-#ifdef RT_POOL_CHECK
-// Diagnostic build (-DRT_POOL_CHECK): consistency checks of the traversal pool (kFPool); a violation
-// is counted and the offending item dropped (no fault), and the counts are printed at rt_scene_free.
-// Build: make single NAME=pc VFLAGS=-DRT_POOL_CHECK; run: RT_LIBRARY=../_lib/librtamd_pc.so pytest
-// tests/test_gpu_parity.py -k pool. [0] item taken with an invalid state ([5] node, [6] stack depth,
-// [7] owner out of range), [1] owner collected another traversal's item, [2] owner collected a
-// result with an invalid hit code, [3] items served, [4] items served by a wave other than their
-// owner, [8] / [9] ready / done bits already set at posting, [10] a taken bit already cleared,
-// [11] a taken item already done, [13] an LDS stack push past stack_depth. (This build found the
-// sign-extended ready mask, bvh_pool's ready_all.)
-__device__ unsigned g_pool_check[16];
-// the first anomaly of a run: (type << 24) | (block << 2) | wave
-__device__ unsigned g_pool_first;
-RT_DEV void pool_anomaly(uint32_t type, uint32_t wave) {
-    atomicAdd(&g_pool_check[type], 1u);
-    atomicCAS(&g_pool_first, 0u, (type << 24) | (blockIdx.x << 2) | wave);
-}
-__device__ unsigned g_pool_dump[24];
-#endif
 // ---------------------------------------------------------------------------
 // vector math, glam 0.22 evaluation order
 // ---------------------------------------------------------------------------
@@ -509,36 +486,6 @@ constexpr uint32_t kFBvh = 1u, kFTri = 2u, kFRuns = 4u, kFDeep = 8u, kFLeafRM = 
 // are 5-8% slower with it (C3 124 -> 133 ms, C5 152 -> 160 ms), so only that preset uses it.
 constexpr uint32_t kFSusp = 64u;
 [[maybe_unused]] constexpr uint32_t kStackLdsMax = 19u;  // LDS stack entries per lane at most (9.5 KB per wave: 16 waves/CU)
-// kFPool (a strategy, like kFSusp): the cross-wave traversal pool. A kFPool instance runs in
-// workgroups of kPoolWaves waves that share their LDS. At a top-level BVH entry each wave traverses
-// until at most kPoolPost of its lanes are still traversing; those lanes post their traversal state
-// (ray, 1/d, t range, best candidate, next node, stack depth, stack owner) into the workgroup's pool,
-// and the wave holding the pool's token runs posted traversals in its idle lanes, refilling them as
-// traversals finish (a traversal's stack stays in its owner's LDS column / HBM spill slab,
-// Trav::sid), while a posting wave that finds the token taken sleeps until its items are done
-// (bvh_pool). A traversal's node visits, leaf tests and their order are exactly the ones its owner
-// would have made (only the lane that executes them changes), so the bits are the same; traversal
-// tails that ran at a few lanes in several waves (C3: 11-17 lanes per BVH trip) run together in one.
-// No barrier: the waves of a workgroup never wait for one another except for posted items.
-constexpr uint32_t kFPool = 128u;
-constexpr uint32_t kPoolWaves = 4u;     // waves per workgroup of a kFPool instance
-#ifndef RT_POOL_POST
-#define RT_POOL_POST 16
-#endif
-constexpr uint32_t kPoolPost = RT_POOL_POST;  // a wave posts its traversals once this few lanes still traverse
-constexpr uint32_t kPoolCap = kPoolWaves * kPoolPost;  // item slots: kPoolPost per wave (<= 64: the ready mask)
-static_assert(kPoolCap <= 64u && kPoolPost <= 32u, "ready / done masks: one 32-bit word per wave, 64 slots");
-constexpr uint32_t kPoolWords = 18u;    // LDS words per item (structure of arrays: word w of item i at w * kPoolCap + i)
-#ifndef RT_POOL_REFILL
-#define RT_POOL_REFILL 48
-#endif
-constexpr uint32_t kPoolRefill = RT_POOL_REFILL;  // the server refills its lanes once this few are still busy
-#ifndef RT_POOL_STACK
-#define RT_POOL_STACK 19
-#endif
-[[maybe_unused]] constexpr uint32_t kPoolStackLds = RT_POOL_STACK;  // LDS stack entries per lane (more: HBM)
-// pool area: the items, then per wave a ready and a done mask word, then the server token
-constexpr uint32_t kPoolLdsWords = kPoolWords * kPoolCap + 2u * kPoolWaves + 1u;
 // One leaf (primitive or cube). tmax = closest so far; a hit with t == closest is
 // accepted, so later candidates win ties exactly like hittable.rs:110-116.
 template <uint32_t kF = kFAll>
@@ -984,15 +931,12 @@ RT_DEV void sort2(float& ta, uint32_t& ca, float& tb, uint32_t& cb) {  // branch
 // to an axis plane (a zero direction component) gets t = (k - o) / d = 0 / 0 from
 // a rect whose plane holds its origin, and every comparison against NaN passes
 // (rectangle.rs:36-65); its sample is re-traced by the reference kernel.
-// A BVH traversal's state between visits (bvh_run). A kFPool traversal's stack owner (its LDS
-// column and, for deep stacks, its HBM spill slab) travels beside it as a sid: the global thread
-// id (wave * 64 + lane) of the lane that started it, which may be another wave's lane.
+// A BVH traversal's state between visits (bvh_run).
 struct Trav {
     uint32_t cur, sp, best_rank;
     float tmax_entry;
     bool any;
 };
-RT_DEV uint32_t self_sid() { return blockIdx.x * blockDim.x + threadIdx.x; }
 // Audit build: every completed fast traversal is replayed with the reference recursion
 // (bvh_hit_reference, on the lane's now free LDS stack); disagreements are recorded.
 RT_DEV void trav_audit(const DevScene& S, const f4* wrapper, uint32_t root, const Ray& r, V inv, float tmin,
@@ -1024,7 +968,7 @@ RT_DEV void trav_audit(const DevScene& S, const f4* wrapper, uint32_t root, cons
 constexpr uint32_t kSuspMinTrips = RT_SUSP_MIN_TRIPS;
 template <int kKind, uint32_t kF, bool kSusp>
 RT_DEV bool bvh_run(const DevScene& S, float delta, const f4* wrapper, const Ray& r, V inv, float tmin, float& closest,
-                    uint32_t& hit_code, uint32_t* stk, uint32_t mode, Trav& tv, uint32_t susp, uint32_t sid = 0u);
+                    uint32_t& hit_code, uint32_t* stk, uint32_t mode, Trav& tv, uint32_t susp);
 template <int kKind, uint32_t kF = kFAll>
 RT_DEV bool bvh_hit(const DevScene& S, float delta, uint32_t root, const Ray& r, float tmin, float& closest,
                     uint32_t& hit_code, uint32_t* stk, uint32_t mode, bool& replay) {
@@ -1085,7 +1029,7 @@ RT_DEV bool bvh_hit(const DevScene& S, float delta, uint32_t root, const Ray& r,
 // visit runs differs, so the result is the same bits.
 template <int kKind, uint32_t kF, bool kSusp>
 RT_DEV bool bvh_run(const DevScene& S, float delta, const f4* wrapper, const Ray& r, V inv, float tmin, float& closest,
-                    uint32_t& hit_code, uint32_t* stk, uint32_t mode, Trav& tv, uint32_t susp, uint32_t sid) {
+                    uint32_t& hit_code, uint32_t* stk, uint32_t mode, Trav& tv, uint32_t susp) {
     const float tmax_entry = tv.tmax_entry;
     const bool prune = (__float_as_uint(wrapper[7].w) & rtdev::kBvhPrunable) != 0u || (mode & kModePruneAllExp);
     const float dmi = delta * fmaxf(fmaxf(__builtin_fabsf(inv.x), __builtin_fabsf(inv.y)), __builtin_fabsf(inv.z));
@@ -1096,14 +1040,10 @@ RT_DEV bool bvh_run(const DevScene& S, float delta, const f4* wrapper, const Ray
                                     hnz = inv.z < 0.0f ? 80u : 32u;
     bool any = tv.any;
     uint32_t best_rank = tv.best_rank, sp = tv.sp, cur = tv.cur;
-    // kFDeep: stack entry sp of this traversal in its owner wave's HBM slab. One-wave workgroups
-    // address it from the scalar block index (a per-lane sid costs C4 9%); a pool instance's
-    // traversal may run in another wave's lane, so it carries its owner in Trav::sid.
-    [[maybe_unused]] auto slab = [&](uint32_t spi) -> uint32_t* {
-        if constexpr ((kF & kFPool) != 0u)
-            return S.stack_spill + (((size_t)(sid >> 6) * S.spill_depth + (spi - S.stack_depth)) * 64u + (sid & 63u)) * 2u;
-        else  // (a wave-uniform base and a 32-bit lane offset: the load takes the scalar-base form)
-            return S.stack_spill + (size_t)blockIdx.x * S.spill_depth * 128u + ((spi - S.stack_depth) * 64u + threadIdx.x) * 2u;
+    // kFDeep: stack entry sp of this lane's traversal in its wave's HBM slab, as a wave-uniform base
+    // and a 32-bit lane offset (the load takes the scalar-base form; fewer 64-bit address ops)
+    [[maybe_unused]] auto spill_at = [&](uint32_t spi) -> uint32_t* {
+        return S.stack_spill + (size_t)blockIdx.x * S.spill_depth * 128u + ((spi - S.stack_depth) * 64u + threadIdx.x) * 2u;
     };
     bool finished = true;
     [[maybe_unused]] uint32_t trips = 0;
@@ -1259,14 +1199,11 @@ RT_DEV bool bvh_run(const DevScene& S, float delta, const f4* wrapper, const Ray
         sort2(t1, c1, t2, c2);
         // LDS stack; with kFDeep the entries past stack_depth go to the HBM spill area
         auto push = [&](uint32_t node, float t) {
-#ifdef RT_POOL_CHECK
-            if ((kF & kFPool) && !(kF & kFDeep) && sp >= S.stack_depth) pool_anomaly(13, 0u);
-#endif
             if (!(kF & kFDeep) || sp < S.stack_depth) {
                 stk[sp * 128u] = node;
                 stk[sp * 128u + 64u] = __float_as_uint(t);
             } else {
-                uint32_t* g = slab(sp);
+                uint32_t* g = spill_at(sp);
                 g[0] = node;
                 g[1] = __float_as_uint(t);
             }
@@ -1291,7 +1228,7 @@ RT_DEV bool bvh_run(const DevScene& S, float delta, const f4* wrapper, const Ray
                 cand = stk[sp * 128u];
                 tenter = __uint_as_float(stk[sp * 128u + 64u]);
             } else {
-                const uint32_t* g = slab(sp);
+                const uint32_t* g = spill_at(sp);
                 cand = g[0];
                 tenter = __uint_as_float(g[1]);
             }
@@ -1316,9 +1253,9 @@ RT_DEV bool bvh_run(const DevScene& S, float delta, const f4* wrapper, const Ray
         const uint32_t first = (uint32_t)__builtin_ctzll(__ballot(1));
         for (uint32_t bin = 0; bin < 8u; ++bin) {
             const uint32_t n = (uint32_t)__popcll(__ballot(b == bin));
-            if (__lane_id() == first && n) atomicAdd(&prof_lds[3u * kPrCount + bin], (unsigned long long)n);
+            if (__lane_id() == first && n) prof_lds[3u * kPrCount + bin] += n;
         }
-        if (__lane_id() == first) atomicAdd(&prof_lds[3u * kPrCount + 8u + trips_bin(m)], 1ull);
+        if (__lane_id() == first) prof_lds[3u * kPrCount + 8u + trips_bin(m)] += 1u;
     }
 #endif
     return finished;
@@ -1906,300 +1843,6 @@ RT_DEV bool world_hit(const DevScene& S, float delta, const Ray& r, Rng& g, cons
     return any;
 }
 
-// One top-level BVH entry (hittable.rs:110-116 for a Bvh, bvh.rs:212-217, 363-417) through the
-// workgroup's traversal pool (kFPool, above); no barrier: the waves of a workgroup stay independent.
-// Phase 1: the wave traverses until at most kPoolPost of its lanes are still traversing. Those lanes
-// post their state into the wave's own kPoolPost item slots and set their bits in the workgroup's
-// `ready` mask. Phase 2: one wave at a time is the pool's server (an LDS token): it takes ready items
-// into its idle lanes (its own, and any other wave's posted meanwhile) and runs them, refilling lanes
-// as traversals finish; a finished item's result goes back to its slot and its bit into `done`. A
-// posting wave that finds a server at work sleeps until its items are done; one that finds none
-// becomes the server. The server hands the token back once no item is ready and none of its lanes is
-// busy, and a waiting wave whose items are still ready takes it, so every posted item is served.
-// closest / hit_code / any_out are the lane's walk state, updated like entry_geom_hit does.
-template <uint32_t kF>
-RT_DEV void bvh_pool(const DevScene& S, float delta, const DevEntry* E, const Ray& ray, bool active, float& closest,
-                     uint32_t& hit_code, bool& any_out, uint32_t* lds, uint32_t* stk, uint32_t wave, uint32_t lane,
-                     uint32_t mode, bool& replay) {
-    const uint32_t root = E->payload;
-    const f4* wrapper = S.nodes + (size_t)root * rtdev::kBvhNodeF4;
-    Ray r = ray;
-    const uint32_t ntf = E->ntf;
-    for (uint32_t i = 0; i < ntf; ++i) r = apply_op(E->tf[i], r);
-    const V inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
-    bool mine = false;
-    if (active) {  // bvh_hit's hand-over rule (NaN-prone rays go to the reference kernel)
-        const float ax = __builtin_fabsf(inv.x), ay = __builtin_fabsf(inv.y), az = __builtin_fabsf(inv.z);
-        const bool fast = ax > 0.0f && ax < kInf && ay > 0.0f && ay < kInf && az > 0.0f && az < kInf &&
-                          __builtin_fabsf(r.o.x) < kInf && __builtin_fabsf(r.o.y) < kInf && __builtin_fabsf(r.o.z) < kInf;
-        if (!fast) replay = true;
-        mine = fast;
-    }
-    Trav tv{root, 0u, 0u, closest, false};
-    bool post = false;
-    if (mine) {  // phase 1: the wave's own traversals, until at most kPoolPost lanes still traverse
-        if (bvh_run<0, kF, true>(S, delta, wrapper, r, inv, 0.001f, closest, hit_code, stk, mode, tv, kPoolPost,
-                                 self_sid())) {
-            trav_audit(S, wrapper, root, r, inv, 0.001f, tv, closest, hit_code, stk);
-            any_out = tv.any;
-        } else {
-            post = true;
-        }
-    }
-    const unsigned long long pm = __ballot(post);
-    if (pm == 0ull) return;
-    const uint32_t region = S.stack_depth * 128u;  // LDS words of one wave's stack
-    uint32_t* P = lds + kPoolWaves * region;       // items: word w of slot i at P[w * kPoolCap + i]
-    // per wave w (32-bit LDS words; bit b = slot w * kPoolPost + b): ready[w] = posted, not yet taken;
-    // done[w] = result written back; then the server token (0 = free, w + 1 = wave w serves)
-    uint32_t* ready = P + kPoolWords * kPoolCap;
-    uint32_t* done = ready + kPoolWaves;
-    uint32_t* token = done + kPoolWaves;
-    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(pm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)pm, 0u));
-    const uint32_t slot = wave * kPoolPost + rank;
-    const uint32_t own = (1u << (uint32_t)__popcll(pm)) - 1u;  // this wave's posted slots in its words
-    if (post) {
-        uint32_t* q = P + slot;
-        q[0 * kPoolCap] = __float_as_uint(r.o.x);
-        q[1 * kPoolCap] = __float_as_uint(r.o.y);
-        q[2 * kPoolCap] = __float_as_uint(r.o.z);
-        q[3 * kPoolCap] = __float_as_uint(r.d.x);
-        q[4 * kPoolCap] = __float_as_uint(r.d.y);
-        q[5 * kPoolCap] = __float_as_uint(r.d.z);
-        q[6 * kPoolCap] = __float_as_uint(inv.x);
-        q[7 * kPoolCap] = __float_as_uint(inv.y);
-        q[8 * kPoolCap] = __float_as_uint(inv.z);
-        q[9 * kPoolCap] = __float_as_uint(r.time);
-        q[10 * kPoolCap] = __float_as_uint(tv.tmax_entry);
-        q[11 * kPoolCap] = __float_as_uint(closest);
-        q[12 * kPoolCap] = hit_code;
-        q[13 * kPoolCap] = tv.best_rank | (tv.any ? 0x80000000u : 0u);
-        q[14 * kPoolCap] = tv.cur;
-        q[15 * kPoolCap] = tv.sp;
-        q[16 * kPoolCap] = self_sid();
-        q[17 * kPoolCap] = root;  // waves run asynchronously: the server may be at another entry
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // the items before their ready bits
-#ifdef RT_POOL_CHECK
-    if (lane == 0u) {
-        if (atomicOr(&ready[wave], own) & own) pool_anomaly(8, wave);  // stale ready bits
-        if (__hip_atomic_load(&done[wave], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & own)
-            pool_anomaly(9, wave);  // stale done bits
-    }
-#else
-    if (lane == 0u) atomicOr(&ready[wave], own);
-#endif
-    // phase 2: serve the pool while this wave holds the token, else wait for the own items
-    bool server = false, busy = false;
-    uint32_t item = 0u, phit = 0u, proot = 0u, psid = 0u;
-    float pclose = 0.0f;
-    Ray pr{};
-    V pinv = mk(0.0f, 0.0f, 0.0f);
-    Trav ptv{};
-    uint32_t* pstk = stk;
-    for (;;) {
-        // the ready slots of all waves as one mask (bit w * kPoolPost + b)
-        auto ready_all = [&]() {
-            unsigned long long m = 0ull;
-            for (uint32_t w = 0; w < kPoolWaves; ++w)
-                m |= (unsigned long long)__hip_atomic_load(&ready[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
-                     << (w * kPoolPost);
-            // (readfirstlane returns int: widen through uint32_t, a sign-extended low word
-            // would show every slot of waves 2-3 ready whenever slot 31 is)
-            return (unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)m) |
-                   ((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(m >> 32)) << 32);
-        };
-        if (!server) {  // take the token when it is free and work is ready
-            uint32_t got = 0u;
-            if (ready_all() != 0ull && lane == 0u) {
-                uint32_t expect = 0u;
-                got = __hip_atomic_compare_exchange_strong(token, &expect, wave + 1u, __ATOMIC_ACQUIRE, __ATOMIC_RELAXED,
-                                                           __HIP_MEMORY_SCOPE_WORKGROUP)
-                          ? 1u
-                          : 0u;
-            }
-            server = __builtin_amdgcn_readfirstlane(got) != 0u;
-            // the previous server's clears happened before its release of the token: no ready
-            // snapshot from before the acquisition may be reused (it may hold items served since)
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        }
-        unsigned long long left = 0ull;  // items still ready after this refill
-        if (server) {  // refill the idle lanes with ready items (only the server clears ready bits)
-            const unsigned long long idle = __ballot(!busy);
-            unsigned long long take = 0ull;
-            if (idle) {
-                unsigned long long m = ready_all();
-                for (uint32_t k = (uint32_t)__popcll(idle); k != 0u && m != 0ull; --k) {
-                    const unsigned long long bit = m & (0ull - m);
-                    take |= bit;
-                    m &= m - 1ull;
-                }
-                left = m;
-                if (take) {
-                    if (lane < kPoolWaves) {
-                        const uint32_t tw = (uint32_t)(take >> (lane * kPoolPost)) & ((1u << kPoolPost) - 1u);
-#ifdef RT_POOL_CHECK
-                        if (tw && (atomicAnd(&ready[lane], ~tw) & tw) != tw) pool_anomaly(10, wave);
-                        if (tw && (__hip_atomic_load(&done[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & tw))
-                            pool_anomaly(11, wave);
-#else
-                        if (tw) atomicAnd(&ready[lane], ~tw);
-#endif
-                    }
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-                    // the r-th idle lane takes the r-th taken slot
-                    const uint32_t ir = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
-                                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
-                    uint32_t it = kPoolCap;
-                    unsigned long long t = take;
-                    for (uint32_t j = 0; t != 0ull; ++j) {
-                        const uint32_t bpos = (uint32_t)__builtin_ctzll(t);
-                        t &= t - 1ull;
-                        if (!busy && ir == j) it = bpos;
-                    }
-                    if (!busy && it < kPoolCap) {
-                        const uint32_t* q = P + it;
-                        pr.o = mk(__uint_as_float(q[0 * kPoolCap]), __uint_as_float(q[1 * kPoolCap]),
-                                  __uint_as_float(q[2 * kPoolCap]));
-                        pr.d = mk(__uint_as_float(q[3 * kPoolCap]), __uint_as_float(q[4 * kPoolCap]),
-                                  __uint_as_float(q[5 * kPoolCap]));
-                        pinv = mk(__uint_as_float(q[6 * kPoolCap]), __uint_as_float(q[7 * kPoolCap]),
-                                  __uint_as_float(q[8 * kPoolCap]));
-                        pr.time = __uint_as_float(q[9 * kPoolCap]);
-                        pclose = __uint_as_float(q[11 * kPoolCap]);
-                        phit = q[12 * kPoolCap];
-                        const uint32_t br = q[13 * kPoolCap];
-                        ptv = Trav{q[14 * kPoolCap], q[15 * kPoolCap], br & 0x7fffffffu, __uint_as_float(q[10 * kPoolCap]),
-                                   (br >> 31) != 0u};
-                        psid = q[16 * kPoolCap];
-                        // the owner's stack column: wave (sid >> 6) & 3 of this workgroup, lane sid & 63
-                        pstk = lds + ((psid >> 6) & (kPoolWaves - 1u)) * region + (psid & 63u);
-                        proot = q[17 * kPoolCap];
-                        item = it;
-                        busy = true;
-#ifdef RT_POOL_CHECK
-                        atomicAdd(&g_pool_check[3], 1u);
-                        if (((psid >> 6) & 3u) != wave) atomicAdd(&g_pool_check[4], 1u);
-                        const bool bad_cur = (ptv.cur & ~rtdev::kLeafNodeFlag) >= S.num_nodes;
-                        const bool bad_sp = ptv.sp > S.stack_depth + S.spill_depth;
-                        const bool bad_sid = (psid >> 8) != blockIdx.x || it / kPoolPost != ((psid >> 6) & 3u);
-                        if (bad_cur) atomicAdd(&g_pool_check[5], 1u);
-                        if (bad_sp) atomicAdd(&g_pool_check[6], 1u);
-                        if (bad_sid) atomicAdd(&g_pool_check[7], 1u);
-                        if (bad_cur || bad_sp || bad_sid) {
-                            atomicCAS(&g_pool_first, 0u, (12u << 24) | (blockIdx.x << 2) | wave);
-                            if (atomicAdd(&g_pool_check[0], 1u) == 0u) {
-                                for (uint32_t w = 0; w < 17u; ++w) g_pool_dump[w] = (P + it)[w * kPoolCap];
-                                g_pool_dump[17] = it;
-                                g_pool_dump[18] = blockIdx.x;
-                                g_pool_dump[19] = wave;
-                                g_pool_dump[20] = ready[0];
-                                g_pool_dump[21] = ready[1];
-                                g_pool_dump[22] = ready[2];
-                                g_pool_dump[23] = ready[3];
-                            }
-                            uint32_t* q2 = P + it;
-                            q2[11 * kPoolCap] = __float_as_uint(ptv.tmax_entry);
-                            q2[12 * kPoolCap] = 0u;
-                            q2[13 * kPoolCap] = 0u;
-                            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                            atomicOr(&done[it / kPoolPost], 1u << (it % kPoolPost));
-                            busy = false;
-                        }
-#endif
-                    }
-                }
-            }
-        }
-        if (__ballot(busy) != 0ull) {
-            if (busy) {
-                const f4* pwrap = S.nodes + (size_t)proot * rtdev::kBvhNodeF4;
-                if (bvh_run<0, kF, true>(S, delta, pwrap, pr, pinv, 0.001f, pclose, phit, pstk, mode, ptv,
-                                         left ? kPoolRefill : 0u, psid)) {
-                    trav_audit(S, pwrap, proot, pr, pinv, 0.001f, ptv, pclose, phit, pstk);
-                    uint32_t* q = P + item;
-                    q[11 * kPoolCap] = __float_as_uint(pclose);
-                    q[12 * kPoolCap] = phit;
-                    q[13 * kPoolCap] = ptv.best_rank | (ptv.any ? 0x80000000u : 0u);
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // the result before its done bit
-                    atomicOr(&done[item / kPoolPost], 1u << (item % kPoolPost));
-                    busy = false;
-                }
-            }
-            continue;
-        }
-        // no lane busy: hand the token back when nothing is ready, leave once the own items are done
-        const uint32_t d = __builtin_amdgcn_readfirstlane(
-            __hip_atomic_load(&done[wave], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-        const bool mine_done = (d & own) == own;
-        if (server && ready_all() == 0ull) {
-            if (lane == 0u) __hip_atomic_store(token, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-            server = false;
-        }
-        if (mine_done && !server) break;
-        if (!server) __builtin_amdgcn_s_sleep(2);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    if (post) {  // the owner takes its traversal's result
-        const uint32_t* q = P + slot;
-        closest = __uint_as_float(q[11 * kPoolCap]);
-        hit_code = q[12 * kPoolCap];
-        any_out = (q[13 * kPoolCap] >> 31) != 0u;
-#ifdef RT_POOL_CHECK
-        if (q[16 * kPoolCap] != self_sid()) atomicAdd(&g_pool_check[1], 1u);
-        if (any_out && (!(hit_code & rtdev::kLeafBit) || rtdev::leaf_index(hit_code) > 0x00ffffffu)) {
-            atomicAdd(&g_pool_check[2], 1u);
-            any_out = false;
-        }
-#endif
-    }
-    if (lane == 0u) atomicAnd(&done[wave], ~own);
-}
-
-// HittableList::hit over the world (hittable.rs:100-118) for kFPool instances: world_hit, with
-// every top-level BVH entry going through bvh_pool. Every wave calls it each sample-loop trip
-// (uniform control flow; `active` lanes have a segment to trace), so the waves of a workgroup
-// meet the same pool calls in the same order.
-template <uint32_t kF>
-RT_DEV bool world_hit_pool(const DevScene& S, float delta, const Ray& r, bool active, Rng& g, const Key& k,
-                           float& t_hit, uint32_t& hit_entry, uint32_t& hit_code, uint32_t* lds, uint32_t* stk,
-                           uint32_t wave, uint32_t lane, uint32_t mode, bool& replay) {
-    float closest = kInf;
-    bool any = false;
-    for (uint32_t e = 0; e < S.num_top; ++e) {
-        const DevEntry* E = S.entries + e;
-        if (E->kind == rtdev::kEntBvh) {
-            bool h = false;
-            uint32_t code = hit_code;
-            bvh_pool<kF>(S, delta, E, r, active, closest, code, h, lds, stk, wave, lane, mode, replay);
-            if (h) {
-                hit_entry = e;
-                hit_code = code;
-                any = true;
-            }
-        } else if (active) {
-            if (E->kind == rtdev::kEntMedium) {
-                float t;
-                if (medium_hit<0, kF>(S, delta, E, r, 0.001f, closest, g, k, t, stk, mode, replay)) {
-                    closest = t;
-                    hit_entry = e;
-                    hit_code = rtdev::leaf_code(rtdev::kLeafMedium, 0);
-                    any = true;
-                }
-            } else {
-                uint32_t code;
-                if (entry_geom_hit<0, kF>(S, delta, E, r, 0.001f, closest, code, stk, mode, replay)) {
-                    hit_entry = e;
-                    hit_code = code;
-                    any = true;
-                }
-            }
-        }
-    }
-    t_hit = closest;
-    return any;
-}
-
 // The suspending list walk of the fast kernel (instances with kFSusp): hittable.rs:100-118 per lane from
 // its own position. A lane's walk state survives the trips of the sample loop: when a BVH
 // traversal is suspended (bvh_run<.., true>: at most `susp` lanes of the wave were left in
@@ -2359,9 +2002,8 @@ RT_DEV bool take_sample(ItemPool& pool, bool want, const DevCamera& C, const Dev
                         const Key& k, unsigned* counter, const ReplayItem* list, uint32_t list_n,
                         TraceCounters* ctr, uint32_t stream_grid, float* sbuf,
                         uint32_t lane, uint32_t& slot, uint32_t& s_local, V& L, V& T, uint32_t& depth, Rng& g,
-                        Ray& ray, uint32_t wg_waves) {
+                        Ray& ray) {
     bool got = false;
-    const uint32_t nwaves = gridDim.x * wg_waves;  // waves of the launch (wg_waves: a compile-time 1 or kPoolWaves)
     for (;;) {
         unsigned long long need = __ballot(want && !got);
         if (need == 0ull || pool.exhausted) break;
@@ -2378,7 +2020,7 @@ RT_DEV bool take_sample(ItemPool& pool, bool want, const DevCamera& C, const Dev
                 if (lane == 0u) {
                     const uint32_t n = __hip_atomic_load(&ctr->replay_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     const uint32_t pl = __hip_atomic_load(&ctr->replay_pull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    lim += (n > pl ? n - pl : 0u) / nwaves;
+                    lim += (n > pl ? n - pl : 0u) / gridDim.x;
                 }
                 lim = __builtin_amdgcn_readfirstlane(lim);
                 if (64u - (uint32_t)__popcll(need) >= lim) break;
@@ -2391,13 +2033,13 @@ RT_DEV bool take_sample(ItemPool& pool, bool want, const DevCamera& C, const Dev
                     role_event(bt);
 #endif
                 } else if (list) {  // a share of the list per wave: a replayed path runs with few others
-                    cnt = (list_n + nwaves - 1u) / nwaves;
+                    cnt = (list_n + gridDim.x - 1u) / gridDim.x;
                     cnt = cnt > 64u ? 64u : cnt;
                     bt = atomicAdd(counter, cnt);
                 } else {
                     const uint32_t cur = __hip_atomic_load(counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     const uint32_t rem = cur < Q.units ? Q.units - cur : 0u;
-                    cnt = rem / (Q.guide * nwaves);
+                    cnt = rem / (Q.guide * gridDim.x);
                     cnt = cnt < 1u ? 1u : (cnt > Q.group ? Q.group : cnt);
                     bt = atomicAdd(counter, cnt);
                 }
@@ -2602,27 +2244,17 @@ constexpr uint32_t kSuspLanes = RT_SUSPEND;  // suspend a BVH traversal's tail a
 // is the default; the fast kernel also exists at 4 (<= 128 VGPRs, a few spills),
 // launched when the scene's LDS stack fits four waves per SIMD (rt_render_launch).
 template <int kKind, int kWaves = 3, uint32_t kF = kFAll>
-__global__ __launch_bounds__((kF & kFPool) != 0u ? 64u * kPoolWaves : 64u, kWaves) void trace_samples(DevScene Sg, DevCamera C, DevParams P, ChunkParams Q,
+__global__ __launch_bounds__(64, kWaves) void trace_samples(DevScene Sg, DevCamera C, DevParams P, ChunkParams Q,
                                                     float* __restrict__ sbuf, TraceCounters* __restrict__ ctr,
                                                     ReplayItem* __restrict__ replay_list, uint32_t fixup,
                                                     unsigned long long* __restrict__ seg_counter) {
     extern __shared__ uint32_t lds_stack[];
-    // kFPool instances run kPoolWaves waves per workgroup (one stack region per wave, then the
-    // pool); every other instance one wave per workgroup
-    // (one-wave instances keep the plain thread index: the pool's wave split costs them registers)
-    constexpr uint32_t wg_waves = (kF & kFPool) != 0u ? kPoolWaves : 1u;
-    const uint32_t lane = wg_waves > 1u ? threadIdx.x & 63u : threadIdx.x;
-    const uint32_t wave = wg_waves > 1u ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : 0u;
-    DevScene S = Sg;
-    uint32_t* stk = lds_stack + wave * S.stack_depth * 128u + lane;  // [level][{node, t_enter}][lane]
-    if constexpr ((kF & kFPool) != 0u) {  // the pool's masks and token start clear
-        if (threadIdx.x < 2u * kPoolWaves + 1u)
-            lds_stack[kPoolWaves * S.stack_depth * 128u + kPoolWords * kPoolCap + threadIdx.x] = 0u;
-        __syncthreads();
-    }
+    const uint32_t lane = threadIdx.x;
+    uint32_t* stk = lds_stack + lane;  // [level][{node, t_enter}][lane]
     // Perlin permutation tables (Marble) behind the stack when they fit: the
     // three dependent byte lookups per lattice corner then hit LDS, not L2.
-    if (!(kF & kFPool) && S.perm_bytes != 0u && S.perm_bytes <= kPermLdsMax && !(P.tune & kModeNoPermLds)) {
+    DevScene S = Sg;
+    if (S.perm_bytes != 0u && S.perm_bytes <= kPermLdsMax && !(P.tune & kModeNoPermLds)) {
         uint32_t* tab = lds_stack + S.stack_depth * 128u;
         const uint32_t* src = reinterpret_cast<const uint32_t*>(Sg.perm);
         for (uint32_t i = lane; i < S.perm_bytes / 4u; i += 64u) tab[i] = src[i];
@@ -2690,7 +2322,7 @@ __global__ __launch_bounds__((kF & kFPool) != 0u ? 64u * kPoolWaves : 64u, kWave
         for (;;) {
             PROF_T0(pr);
             if (take_sample(pool, !has, C, P, Q, k, counter, list, list_n, ctr, stream_grid, sbuf, lane, slot, take_sample_idx, L, T, depth, g,
-                            ray, wg_waves)) {
+                            ray)) {
                 has = true;
                 w.pos = 0u;
                 w.resume = false;
@@ -2728,13 +2360,11 @@ __global__ __launch_bounds__((kF & kFPool) != 0u ? 64u * kPoolWaves : 64u, kWave
     for (;;) {
         PROF_T0(pr);
         if (take_sample(pool, !has, C, P, Q, k, counter, list, list_n, ctr, stream_grid, sbuf, lane, slot, take_sample_idx, L, T, depth, g,
-                        ray, wg_waves)) {
+                        ray)) {
             has = true;
         }
         PROF_ADD(kPrRefill, pr);
-        if (__ballot(has) == 0ull) {
-            break;  // pool exhausted and every path finished
-        }
+        if (__ballot(has) == 0ull) break;  // pool exhausted and every path finished
 #ifdef RT_PROFILE_REGIONS
         if (kKind == 0) {  // throughput histogram: this iteration's segments into the current bucket
             const uint32_t b = (uint32_t)((__builtin_amdgcn_s_memrealtime() - wave_t0) / kTpTicks);
@@ -2746,33 +2376,7 @@ __global__ __launch_bounds__((kF & kFPool) != 0u ? 64u * kPoolWaves : 64u, kWave
             tp_acc += (uint32_t)__popcll(__ballot(has));
         }
 #endif
-        if constexpr ((kF & kFPool) != 0u) {  // every wave walks the world, active lanes with a segment
-            bool replay = false, any = false;
-            float t = 0.0f;
-            uint32_t he = 0, hc = 0;
-            PROF_T0(pw);
-            any = world_hit_pool<kF>(S, P.prune_delta, ray, has, g, k, t, he, hc, lds_stack, stk, wave, lane, mode,
-                                     replay);
-            PROF_ADD(kPrWorld, pw);
-            bool shade = has;
-            if (has && replay) {  // hand the sample to the reference kernel
-                unsigned idx = atomicAdd(&ctr->replay_count, 1u);
-                if (idx < kReplayCap) replay_publish(replay_list, idx, g.pixel, g.sample - Q.sample0);
-                has = false;
-                shade = false;
-            }
-            if constexpr ((kF & kFMarble) != 0u) {
-                if (shade_marble<kF>(S, P, Q, k, sbuf, shade, any, he, hc, t, ray, L, T, depth, g, slot,
-                                     g.sample - Q.sample0)) {
-                    has = false;
-                    nseg += P.max_depth - depth + (depth != 0u ? 1u : 0u);
-                }
-            } else if (shade && finish_segment<kF>(S, P, Q, k, sbuf, any, he, hc, t, ray, L, T, depth, g, slot,
-                                                   g.sample - Q.sample0)) {
-                has = false;
-                nseg += P.max_depth - depth + (depth != 0u ? 1u : 0u);
-            }
-        } else if constexpr ((kF & kFMarble) != 0u) {
+        if constexpr ((kF & kFMarble) != 0u) {
             bool shade = false, any = false;
             float t = 0.0f;
             uint32_t he = 0, hc = 0;
@@ -2826,16 +2430,13 @@ __global__ __launch_bounds__((kF & kFPool) != 0u ? 64u * kPoolWaves : 64u, kWave
         __threadfence();  // (release: its replay-list entries and replay_count increments first)
         atomicAdd(&ctr->fast_done, 1u);
     }
-#ifdef RT_PROFILE_REGIONS
-    if constexpr ((kF & kFPool) != 0u) __syncthreads();  // every wave of the workgroup has counted
-#endif
     PROF_FLUSH();
 #ifdef RT_PROFILE_REGIONS
     if (kKind == 0 && lane == 0u && tp_acc && tp_bucket < kTpBuckets) atomicAdd(&g_tp_hist[tp_bucket], tp_acc);
     if (stream_grid && lane == 0u) role_event(0xfffffffeu);
-    if (kKind == 0 && lane == 0u && (self_sid() >> 6) < kProfWaves) {
-        g_wave_t[2u * (self_sid() >> 6)] = wave_t0;
-        g_wave_t[2u * (self_sid() >> 6) + 1u] = __builtin_amdgcn_s_memrealtime();
+    if (kKind == 0 && lane == 0u && blockIdx.x < kProfWaves) {
+        g_wave_t[2u * blockIdx.x] = wave_t0;
+        g_wave_t[2u * blockIdx.x + 1u] = __builtin_amdgcn_s_memrealtime();
     }
 #endif
 }
@@ -2940,10 +2541,6 @@ __global__ void kat_eval(int op, const float* __restrict__ in, float* __restrict
 void* rt_mc_trace_instance(uint32_t preset) {
     if (preset == kFBvh) return reinterpret_cast<void*>(trace_samples<0, 4, kFBvh>);
     if (preset == (kFBvh | kFMarble)) return reinterpret_cast<void*>(trace_samples<0, 4, kFBvh | kFMarble>);
-    if (preset == (kFBvh | kFMarble | kFPool))
-        return reinterpret_cast<void*>(trace_samples<0, 4, kFBvh | kFMarble | kFPool>);
-    if (preset == (kFBvh | kFMarble | kFPool | kFDeep))
-        return reinterpret_cast<void*>(trace_samples<0, 4, kFBvh | kFMarble | kFPool | kFDeep>);
     if (preset == kFRuns) return reinterpret_cast<void*>(trace_samples<0, 4, kFRuns>);
     return nullptr;
 }
@@ -3057,8 +2654,7 @@ using TraceKernel = void (*)(DevScene, DevCamera, DevParams, ChunkParams, float*
 template <int kWaves, uint32_t kF>
 TraceKernel preset_instance() {
 #ifdef RT_SPLIT_MC
-    if constexpr (kWaves == 4 && (kF == kFBvh || kF == (kFBvh | kFMarble) || kF == (kFBvh | kFMarble | kFPool) ||
-                                  kF == (kFBvh | kFMarble | kFPool | kFDeep) || kF == kFRuns))
+    if constexpr (kWaves == 4 && (kF == kFBvh || kF == (kFBvh | kFMarble) || kF == kFRuns))
         return reinterpret_cast<TraceKernel>(rt_mc_trace_instance(kF));
     else if constexpr (kF == 0u)
         return reinterpret_cast<TraceKernel>(rt_flat_trace_instance(kWaves));
@@ -3071,11 +2667,6 @@ TraceKernel fast_instance(uint32_t features) {
     if (features == 0u) return preset_instance<kWaves, 0u>();
     if ((features & ~kFRuns) == 0u) return preset_instance<kWaves, kFRuns>();
     if ((features & ~kFBvh) == 0u) return preset_instance<kWaves, kFBvh>();
-    if constexpr (kWaves == 4) {  // the traversal pool (kFPool) instances of the sphere-BVH + Marble preset
-        if (features == (kFBvh | kFMarble | kFPool)) return preset_instance<4, kFBvh | kFMarble | kFPool>();
-        if (features == (kFBvh | kFMarble | kFPool | kFDeep))
-            return preset_instance<4, kFBvh | kFMarble | kFPool | kFDeep>();
-    }
     if ((features & ~(kFBvh | kFMarble)) == 0u) return preset_instance<kWaves, kFBvh | kFMarble>();
     if ((features & ~(kFBvh | kFTri | kFDeep)) == 0u) return preset_instance<kWaves, kFBvh | kFTri | kFDeep | kFSusp>();
     return preset_instance<kWaves, kFAll>();
@@ -3227,16 +2818,9 @@ int rt_scene_upload(const rt_scene_desc* desc, int device, rt_scene_handle* out)
     s->features = (hs.tri.empty() ? 0u : kFTri) | (hs.bvh_rect_msph ? kFLeafRM : 0u);
     for (const rtdev::DevTexture& t : hs.texs)
         if (t.kind == rtdev::kTexMarble) s->features |= kFMarble;
-    for (const rtdev::DevEntry& e : hs.entries) {  // top-level entries and medium boundaries
-        if (e.kind == rtdev::kEntBvh) s->features |= kFBvh;
-        if (e.kind == rtdev::kEntSphereRun && e.pad[0] >= kRunPretestMin) s->features |= kFRuns;
-    }
-    // RT_OPT_TUNE's kModePool (A/B, tests): the sphere-BVH + Marble preset through the workgroup pool
-    const bool pool = s->features == (kFBvh | kFMarble) && (opt(RT_OPT_TUNE) & kModePool);
-    if (pool) s->features |= kFPool;
 #ifndef RT_LEAF_AUDIT  // (the audit build replays traversals on the same LDS stack: no spill area)
-    {  // deep BVHs: the LDS stack keeps kStackLdsMax entries (kPoolStackLds in pool instances), HBM the rest
-        uint32_t cap = pool ? kPoolStackLds : kStackLdsMax;
+    {  // deep BVHs: the LDS stack keeps kStackLdsMax entries, HBM the rest
+        uint32_t cap = kStackLdsMax;
         if (const int64_t v = opt(RT_OPT_STACK_LDS))  // diagnostics / tests: a smaller LDS part (>= 1)
             cap = std::min(cap, (uint32_t)v);
         if (hs.max_stack > cap) {
@@ -3246,6 +2830,10 @@ int rt_scene_upload(const rt_scene_desc* desc, int device, rt_scene_handle* out)
         }
     }
 #endif
+    for (const rtdev::DevEntry& e : hs.entries) {  // top-level entries and medium boundaries
+        if (e.kind == rtdev::kEntBvh) s->features |= kFBvh;
+        if (e.kind == rtdev::kEntSphereRun && e.pad[0] >= kRunPretestMin) s->features |= kFRuns;
+    }
     uint64_t c[10] = {hs.entries.size(), hs.sph.size(), hs.msph.size() / 3, hs.rect.size() / 2, hs.tri.size() / 3,
                       hs.nodes.size() / rtdev::kBvhNodeF4, hs.mats.size(), hs.texs.size(), hs.max_bvh_depth, total};
     memcpy(s->counts, c, sizeof c);
@@ -3349,25 +2937,6 @@ int rt_scene_free(rt_scene_handle s) {
         }
         if (hipMemcpyFromSymbol(&na, HIP_SYMBOL(g_bounds_audit_count), sizeof na) == hipSuccess)
             fprintf(stderr, "{\"bounds_audit_count\": %u}\n", na);
-#endif
-#ifdef RT_POOL_CHECK
-        {
-            unsigned first = 0;
-            if (hipMemcpyFromSymbol(&first, HIP_SYMBOL(g_pool_first), sizeof first) == hipSuccess)
-                fprintf(stderr, "{\"pool_first\": [%u, %u, %u]}\n", first >> 24, (first & 0xffffffu) >> 2, first & 3u);
-            unsigned pc[16] = {};
-            if (hipDeviceSynchronize() == hipSuccess && hipMemcpyFromSymbol(pc, HIP_SYMBOL(g_pool_check), sizeof pc) == hipSuccess) {
-                fprintf(stderr, "{\"pool_check\": [");
-                for (int i = 0; i < 16; ++i) fprintf(stderr, "%s%u", i ? ", " : "", pc[i]);
-                fprintf(stderr, "]}\n");
-            }
-            unsigned dump[24] = {};
-            if (hipMemcpyFromSymbol(dump, HIP_SYMBOL(g_pool_dump), sizeof dump) == hipSuccess) {
-                fprintf(stderr, "{\"pool_dump\": [");
-                for (int i = 0; i < 24; ++i) fprintf(stderr, "%s%u", i ? ", " : "", dump[i]);
-                fprintf(stderr, "]}\n");
-            }
-        }
 #endif
         if (s->done) (void)hipEventSynchronize(s->done);  // the last launch may still use the buffers below
         if (s->pool) (void)hipFree(s->pool);
@@ -3572,19 +3141,14 @@ int rt_render_launch_camera(rt_scene_handle s, const rt_camera* camera, const rt
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per3, k3, 64, stack_lds + perm3) != hipSuccess) per3 = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per4, k4, 64, stack_lds) != hipSuccess) per4 = 0;
         s->fast_waves = per4 > per3 && !(dp.tune & kModeW3) && !prefer3 ? 4 : 3;
-        if (s->features & kFPool) s->fast_waves = 4;  // (pool instances exist at four waves per SIMD)
     }
-    // kFPool instances run kPoolWaves waves per workgroup: their stacks, then the pool
-    const bool pool = (s->features & kFPool) != 0u;
-    const uint32_t wg_waves = pool ? kPoolWaves : 1u;
     if (s->fast_waves == 4) dp.tune |= kModeNoPermLds;
     // LDS per wave: the kernel's traversal stack, then the Perlin tables
     DevScene dev_ref = s->dev;
     dev_ref.stack_depth = s->stack_ref;
     const size_t perm_lds =
         s->dev.perm_bytes != 0u && s->dev.perm_bytes <= kPermLdsMax && !(dp.tune & kModeNoPermLds) ? s->dev.perm_bytes : 0u;
-    const size_t lds = pool ? kPoolWaves * (size_t)s->dev.stack_depth * 128u * sizeof(uint32_t) + kPoolLdsWords * 4u
-                            : (size_t)s->dev.stack_depth * 128u * sizeof(uint32_t) + perm_lds;
+    const size_t lds = (size_t)s->dev.stack_depth * 128u * sizeof(uint32_t) + perm_lds;
     size_t lds_ref = (size_t)dev_ref.stack_depth * 128u * sizeof(uint32_t) + perm_lds;
     if ((dp.flags & RT_FLAG_HRPP) && s->dev.hrpp_npred) {  // the experiment: reference kernel + predictors
         dp.flags |= RT_FLAG_EXACT_BVH;
@@ -3613,10 +3177,9 @@ int rt_render_launch_camera(rt_scene_handle s, const rt_camera* camera, const rt
     if (s->grid == 0) {
         int per_cu = 0, per_cu_ref = 0, cus = 0;
         const TraceKernel kf = fast_instance(s->fast_waves, s->features);
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kf, 64 * wg_waves, lds) != hipSuccess ||
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kf, 64, lds) != hipSuccess ||
             per_cu < 1)
-            per_cu = 8 / (int)wg_waves;
-        per_cu *= (int)wg_waves;  // resident waves per CU
+            per_cu = 8;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_ref, trace_samples<1>, 64, lds_ref) != hipSuccess ||
             per_cu_ref < 1)
             per_cu_ref = 8;
@@ -3655,8 +3218,7 @@ int rt_render_launch_camera(rt_scene_handle s, const rt_camera* camera, const rt
         uint32_t grid = (uint32_t)s->grid, grid_ref = (uint32_t)s->grid_ref;
         if (grid > q.units) grid = q.units;
         if (grid_ref > q.units) grid_ref = q.units;
-        const uint32_t fast_blocks = (grid + wg_waves - 1u) / wg_waves;  // workgroups of the fast kernel
-        q.fast_grid = exact || dev_ref.hrpp_tab ? grid : fast_blocks * wg_waves;  // its waves
+        q.fast_grid = grid;
         hipEvent_t* evp = nullptr;
         if (s->ev_count < rt_scene::kEvents) {
             evp = s->ev[s->ev_count];
@@ -3678,8 +3240,8 @@ int rt_render_launch_camera(rt_scene_handle s, const rt_camera* camera, const rt
             const bool kind3 = !(s->features & kFDeep) && !(dp.tune & kModeReplayRef);
             const bool stream_rp = kind3 && !(dp.tune & kModeNoStream);
             if (stream_rp && (e = hipEventRecord(s->fork, st)) != hipSuccess) return hip_fail(e, "replay stream fork");
-            hipLaunchKernelGGL(kf, dim3(fast_blocks), dim3(64 * wg_waves), lds, st, s->dev, cam, dp, q, s->sbuf,
-                               s->counter, s->replay, 0u, d_segments);
+            hipLaunchKernelGGL(kf, dim3(grid), dim3(64), lds, st, s->dev, cam, dp, q, s->sbuf, s->counter, s->replay,
+                               0u, d_segments);
             if (kind3) {
                 // the replay pass: fast traversal except for the rays that were handed over
                 DevScene dev_rp = s->dev;

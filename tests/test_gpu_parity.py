@@ -386,21 +386,6 @@ def test_stack_spill_to_hbm_matches_oracle(cfg_name, rt, orc):
     assert st["segments"] == cnt["segments"]
 
 
-@pytest.mark.parametrize("stack_lds", [0, 2])
-@pytest.mark.parametrize("pool", [True, False])
-def test_traversal_pool_matches_oracle(pool, stack_lds, rt, orc):
-    # RT_OPT_TUNE bit 22 at upload runs the showcase preset's top-level BVHs through the
-    # workgroup pool (kernel.hip kFPool: the tails of four waves' traversals run together in one
-    # wave, each on its owner's stack); without it the one-wave instance runs. Both, and the
-    # pool with a 2-entry LDS stack (every stack mostly in its owner's HBM slab), are the oracle.
-    cfg, scene, params = setup(rt, "C3", 48, 3, seed=13)
-    want, cnt = orc.render(scene, cfg.camera(), params)
-    with rt.options(tune=(1 << 22) if pool else 0, stack_lds=stack_lds):
-        got, st = gpu_render(rt, scene, cfg.camera(), params)
-    np.testing.assert_array_equal(got, want)
-    assert st["segments"] == cnt["segments"]
-
-
 @pytest.mark.parametrize("replay_ref", [False, True])
 @pytest.mark.parametrize("cfg_name,w,h", [("C3", 40, None), ("C5", 41, None), ("C3", 7, 1)])
 def test_replay_pass_kernels_match_oracle(cfg_name, w, h, replay_ref, rt, orc):

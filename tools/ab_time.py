@@ -24,8 +24,8 @@ from raytracinginoneweekendinrust_amd.configs import CONFIGS  # noqa: E402
 
 
 def bind(spec, idx):
-    """spec: path.so, or path.so:0xTUNE (that library's RT_OPT_TUNE bits, e.g. 0x400000 = the traversal
-    pool). Each spec loads its own copy of the file, so one build can be compared with itself."""
+    """spec: path.so, or path.so:0xTUNE (that library's RT_OPT_TUNE bits, e.g. 0x40 = the 3-wave
+    instance). Each spec loads its own copy of the file, so one build can be compared with itself."""
     import shutil
     import tempfile
     path, _, tune = spec.partition(":")

@@ -79,13 +79,6 @@ probe)  # dual-issue rules, the C3 region profile and instruction classes of the
     pmc c3_mix2 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 \
         SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VALU -- $B
     ;;
-pool)  # the traversal pool: its parity test, the GPU suite, A/B against the one-wave instance
-    step pool_test 600 python -u -m pytest tests/test_gpu_parity.py -x -v --timeout 300 --timeout-method thread \
-        -k "traversal_pool"
-    L=raytracinginoneweekendinrust_amd/_lib/librtamd.so
-    step ab_c3 900 python -u tools/ab_time.py --config C3 --spp 100 --reps 3 $L $L:0x400000 $L $L:0x400000
-    gpu_tests
-    ;;
 ab)  # A/B of library builds: bash tools/r03_session.sh ab <config> <spp> lib1.so lib2.so ...
     CFG="$1"; SPP="$2"; shift 2
     step "ab_$CFG" 900 python -u tools/ab_time.py --config "$CFG" --spp "$SPP" --reps 3 "$@"
