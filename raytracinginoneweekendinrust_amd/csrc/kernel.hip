@@ -1040,11 +1040,6 @@ RT_DEV bool bvh_run(const DevScene& S, float delta, const f4* wrapper, const Ray
                                     hnz = inv.z < 0.0f ? 80u : 32u;
     bool any = tv.any;
     uint32_t best_rank = tv.best_rank, sp = tv.sp, cur = tv.cur;
-    // kFDeep: stack entry sp of this lane's traversal in its wave's HBM slab, as a wave-uniform base
-    // and a 32-bit lane offset (the load takes the scalar-base form; fewer 64-bit address ops)
-    [[maybe_unused]] auto spill_at = [&](uint32_t spi) -> uint32_t* {
-        return S.stack_spill + (size_t)blockIdx.x * S.spill_depth * 128u + ((spi - S.stack_depth) * 64u + threadIdx.x) * 2u;
-    };
     bool finished = true;
     [[maybe_unused]] uint32_t trips = 0;
 #ifdef RT_PROFILE_REGIONS
@@ -1203,7 +1198,8 @@ RT_DEV bool bvh_run(const DevScene& S, float delta, const f4* wrapper, const Ray
                 stk[sp * 128u] = node;
                 stk[sp * 128u + 64u] = __float_as_uint(t);
             } else {
-                uint32_t* g = spill_at(sp);
+                uint32_t* g = S.stack_spill +
+                              (((size_t)blockIdx.x * S.spill_depth + (sp - S.stack_depth)) * 64u + threadIdx.x) * 2u;
                 g[0] = node;
                 g[1] = __float_as_uint(t);
             }
@@ -1228,7 +1224,8 @@ RT_DEV bool bvh_run(const DevScene& S, float delta, const f4* wrapper, const Ray
                 cand = stk[sp * 128u];
                 tenter = __uint_as_float(stk[sp * 128u + 64u]);
             } else {
-                const uint32_t* g = spill_at(sp);
+                const uint32_t* g = S.stack_spill +
+                                    (((size_t)blockIdx.x * S.spill_depth + (sp - S.stack_depth)) * 64u + threadIdx.x) * 2u;
                 cand = g[0];
                 tenter = __uint_as_float(g[1]);
             }
