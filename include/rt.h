@@ -250,7 +250,12 @@ int rt_scene_info(rt_scene_handle scene, uint64_t counts[10]);
  * Renders on one scene handle are serialised: a launch waits (on the device,
  * hipStreamWaitEvent) for the previous launch on the same handle to finish,
  * whatever stream either was issued on, because they share the handle's sample
- * buffer and counters; concurrent calls from several threads are safe. */
+ * buffer and counters; concurrent calls from several threads are safe.
+ * Memory: the handle keeps a device sample buffer (12 B per pixel and sample of a
+ * chunk) sized for the largest launch it has run, at most 40% of the HBM free when it
+ * grew (at least 8 GiB; rt_set_option(RT_OPT_SAMPLE_BUFFER_MB) caps it), until
+ * rt_scene_free. Several handles on one device each keep their own: cap the buffer
+ * when many handles share a GPU, or a later one may fall back to more chunks. */
 int rt_render_launch(rt_scene_handle scene, const rt_camera_desc* camera,
                      const rt_render_params* params, float* d_out,
                      unsigned long long* d_segments, void* stream);

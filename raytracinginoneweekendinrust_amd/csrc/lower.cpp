@@ -667,6 +667,10 @@ class Lowerer {
         std::vector<uint8_t> seen(cnt, 0);
         bool prunable = true;
         const Box none{{0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f}};
+        auto inside = [](const Box& c, const Box& p) {
+            return p.mn.x <= c.mn.x && p.mn.y <= c.mn.y && p.mn.z <= c.mn.z && c.mx.x <= p.mx.x && c.mx.y <= p.mx.y &&
+                   c.mx.z <= p.mx.z;
+        };
         // iterative preorder walk from the root: every node reached exactly once
         std::vector<std::pair<uint32_t, uint32_t>> st{{(uint32_t)n.ref[2], 1u}};
         while (!st.empty()) {
@@ -695,6 +699,10 @@ class Lowerer {
                     if (c.kind == RT_OBJ_MOVING_SPHERE || c.kind == RT_OBJ_XY_RECT || c.kind == RT_OBJ_XZ_RECT ||
                         c.kind == RT_OBJ_YZ_RECT)
                         s_->bvh_rect_msph = true;
+                    // Pruning assumes every primitive lies inside the box the caller gave the node
+                    // holding it. The reference only tests those boxes (bvh.rs:363-417), so a tree
+                    // that breaks this is legal; it is traversed without pruning.
+                    if (!inside(prim_box(c, 0.0f, 0.0f), t.box)) prunable = false;
                 }
                 int rc;
                 t.is_node[0] = t.is_node[1] = false;
@@ -720,10 +728,6 @@ class Lowerer {
         // The BVH4 collapse skips the box tests of interior nodes it merges away:
         // exact only when every Index child's box lies inside its parent's (the
         // reference builder's boxes are unions, bvh.rs:294-300, so this holds).
-        auto inside = [](const Box& c, const Box& p) {
-            return p.mn.x <= c.mn.x && p.mn.y <= c.mn.y && p.mn.z <= c.mn.z && c.mx.x <= p.mx.x && c.mx.y <= p.mx.y &&
-                   c.mx.z <= p.mx.z;
-        };
         for (uint32_t i = 0; i < cnt; ++i) {
             if (!seen[i]) return fail(RT_ERR_INVALID, "BVH tree node " + std::to_string(i) + " not reachable from the root");
             for (int k = 0; k < 2; ++k)

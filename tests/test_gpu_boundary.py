@@ -50,6 +50,22 @@ def test_prebuilt_tree_with_moving_spheres_ignores_tree_times(rt, orc):
     assert st["segments"] == cnt["segments"]
 
 
+def test_prebuilt_tree_with_boxes_smaller_than_their_objects(rt, orc):
+    """A caller's leaf boxes need not contain their objects (the reference tests only the
+    boxes, bvh.rs:363-417): a sphere sticking out of its box toward the ray can be hit
+    before that box is entered, so such a tree is lowered without closest-hit pruning."""
+    scene = sphere_scene(rt, n=150, seed=31, tree="median-x", box_scale=0.6)
+    p = rt.render_params(72, 48, 8, 12, background=(0.7, 0.8, 1.0))
+    ds = rt.DeviceScene(scene)
+    try:
+        got, st = ds.render(_cam(rt), p)
+    finally:
+        ds.close()
+    want, cnt = orc.render(scene, _cam(rt), p)
+    np.testing.assert_array_equal(got, want)
+    assert st["segments"] == cnt["segments"]
+
+
 def test_camera_basis_equals_camera_new_on_device(rt):
     cfg = rt.CONFIGS["C3"].scaled(48, 4)
     scene = rt.Scene.generate(cfg.scene, cfg.scene_seed)

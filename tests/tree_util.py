@@ -73,9 +73,12 @@ def build_tree(rt, objs, boxes, rng, split="random"):
     return nodes, root
 
 
-def sphere_scene(rt, n=120, seed=5, tree="random", with_tree=True, cubes=20, moving=0, tree_times=(0.0, 1.0)):
+def sphere_scene(rt, n=120, seed=5, tree="random", with_tree=True, cubes=20, moving=0, tree_times=(0.0, 1.0),
+                 box_scale=1.0):
     """Ground + n spheres (+ cubes, + `moving` moving spheres) in a prebuilt tree (or a flat
-    list when not with_tree); `tree_times` are the f[0] / f[1] the tree node is given."""
+    list when not with_tree); `tree_times` are the f[0] / f[1] the tree node is given.
+    box_scale != 1 scales every leaf box about its centre before the tree is built (boxes
+    that do not contain their primitives: legal for the reference, which tests only boxes)."""
     rng = np.random.default_rng(seed)
     b = rt.SceneBuilder()
     world = rt.HittableList()
@@ -104,6 +107,14 @@ def sphere_scene(rt, n=120, seed=5, tree="random", with_tree=True, cubes=20, mov
         c1 = (float(x), r + float(rng.uniform(0.1, 0.5)), float(z))
         objs.append(b.moving_sphere(c0, c1, 0.0, 1.0, r, b.lambertian_from_color(tuple(rng.uniform(0, 1, 3)))))
         boxes.append(prim_box(K.RT_OBJ_MOVING_SPHERE, (*c0, *c1, 0.0, 1.0, r)))
+    if box_scale != 1.0:
+        sc = np.float32(box_scale)
+        scaled = []
+        for lo, hi in boxes:
+            lo, hi = np.float32(lo), np.float32(hi)
+            c, h = (lo + hi) * np.float32(0.5), (hi - lo) * np.float32(0.5) * sc
+            scaled.append((tuple(c - h), tuple(c + h)))
+        boxes = scaled
     if with_tree:
         nodes, root = build_tree(rt, objs, boxes, rng, tree)
         world.add(b.bvh_tree(nodes, root, *tree_times))
