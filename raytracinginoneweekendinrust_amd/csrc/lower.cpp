@@ -1007,40 +1007,6 @@ class Lowerer {
 
 }  // namespace
 
-void bvh_split_schedule(uint32_t n, uint64_t seed, BvhSchedule* out) {
-    // The recursion of BvhNode::new_helper (bvh.rs:249-333) without the sorting:
-    // one axis draw per node in preorder; nodes of > 2 items split at n / 2.
-    std::vector<std::vector<uint32_t>> lv;  // per depth: start, count, axis triples
-    AxisStream ax(seed);
-    struct Frame {
-        uint32_t start, count, depth;
-    };
-    std::vector<Frame> st;
-    if (n) st.push_back({0u, n, 0u});
-    while (!st.empty()) {
-        Frame f = st.back();
-        st.pop_back();
-        const uint32_t axis = (uint32_t)ax.axis();
-        if (lv.size() <= f.depth) lv.resize(f.depth + 1);
-        lv[f.depth].insert(lv[f.depth].end(), {f.start, f.count, axis});
-        if (f.count > 2) {
-            const uint32_t mid = f.count / 2;
-            st.push_back({f.start + mid, f.count - mid, f.depth + 1});  // right after the left subtree
-            st.push_back({f.start, mid, f.depth + 1});
-        }
-    }
-    *out = BvhSchedule();
-    out->level_off.push_back(0);
-    for (const auto& v : lv) {
-        for (size_t i = 0; i < v.size(); i += 3) {
-            out->start.push_back(v[i]);
-            out->count.push_back(v[i + 1]);
-            out->axis.push_back(v[i + 2]);
-        }
-        out->level_off.push_back((uint32_t)out->start.size());
-    }
-}
-
 int lower_scene(const rt_scene_desc* desc, HostScene* out, std::string* err, const BvhOrderer* orderer) {
     *out = HostScene();
     Lowerer l(desc, out, err, orderer);

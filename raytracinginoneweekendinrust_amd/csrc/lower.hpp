@@ -49,16 +49,6 @@ struct BvhOrderer {
 // Returns RT_OK or a negative rt_status with a message in *err.
 int lower_scene(const rt_scene_desc* desc, HostScene* out, std::string* err, const BvhOrderer* orderer = nullptr);
 
-// The split schedule of one Bvh::new over n items: every node of the reference
-// recursion (its shape depends only on n) with its first item, item count and
-// split axis (drawn in preorder from the BVH's axis stream, bvh.rs:255), grouped
-// by depth; within a depth, nodes are in increasing `start`.
-struct BvhSchedule {
-    std::vector<uint32_t> level_off;  // level L's nodes are [level_off[L], level_off[L + 1])
-    std::vector<uint32_t> start, count, axis;
-};
-void bvh_split_schedule(uint32_t n, uint64_t seed, BvhSchedule* out);
-
 // BvhOrderer::fn backed by rt_bvh_build_order on device *(int*)ctx (bvh_build.hip).
 int device_bvh_order(void* ctx, const float* keys, uint32_t n, uint64_t seed, uint32_t* order, std::string* err);
 
