@@ -289,7 +289,9 @@ int rt_format_ppm(const float* d_rgb, uint32_t width, uint32_t height, char* d_t
  * (random axis per node, stable total_cmp sort, split at n / 2, two-item nodes
  * ordered by one comparison). Synchronises `stream`. rt_scene_upload uses it for
  * BVHs of >= 16384 items (RT_OPT_BVH_BUILD overrides: "device always" builds every
- * BVH on the device, "host always" none); the lowered tree is identical either way. */
+ * BVH on the device, "host always" none); the lowered tree is identical either way.
+ * n < 2^31; RT_ERR_UNSUPPORTED beyond about 1.4e9 items (the split-axis draws would
+ * exceed 2^32 words). Device memory: about 33 B per item for the call's duration. */
 int rt_bvh_build_order(const float* d_keys, uint32_t n, uint64_t seed, uint32_t* d_order, void* stream);
 
 /* Diagnostic options (tests, A/B runs, experiments). The library reads no environment
