@@ -103,6 +103,10 @@ class FrameGather:
         if self.rank != 0 and handle[0] is not None:
             try:
                 self._peer = ipc_open(handle[0], dev)
+                if self.cnt:  # one real peer copy into this rank's slot, so a transport that maps but
+                    from . import copy_async  # cannot copy falls back here, not inside a timed step
+                    copy_async(self._peer + self.off * 4, self.d_pack.data_ptr(), 4, self._stream())
+                    self._sync()
             except Exception:
                 ok = 0
         elif handle[0] is None:
