@@ -289,6 +289,19 @@ def test_full_workload_subsample_matches_oracle(cfg_name, shard, rt, orc):
     assert np.isfinite(got).all()
 
 
+def test_c1_full_frame_matches_oracle(rt, orc):
+    # BASELINE config 1 (random_spheres 400x225, 50 spp, depth 50) in full: every pixel and
+    # the segment count against the oracle's whole frame (4.5 M samples, a few seconds of CPU)
+    import os
+    cfg = rt.CONFIGS["C1"]
+    scene = rt.Scene.generate(cfg.scene, cfg.scene_seed)
+    params = rt.render_params(cfg.width, cfg.height, cfg.spp, cfg.depth, background=cfg.background())
+    got, st = gpu_render(rt, scene, cfg.camera(), params)
+    want, cnt = orc.render(scene, cfg.camera(), params, threads=max(1, min(16, len(os.sched_getaffinity(0)))))
+    np.testing.assert_array_equal(got, want)
+    assert st["segments"] == cnt["segments"]
+
+
 @pytest.mark.parametrize("cfg_name,spp", [("C3", 500), ("C2", 8), ("C1", 16), ("C4", 100)])
 def test_pruned_traversal_equals_reference_traversal_full_frame(cfg_name, spp, rt):
     # Closest-hit box pruning and leaf-box rejects must not change a single path:
