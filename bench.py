@@ -9,9 +9,10 @@ One step = one whole C3 frame (showcase, 1200x800, 500 spp, depth 50) with the
 scene already resident in HBM. At N GPUs (one process each) the
 frame is fixed (strong scaling, the north-star workload): rank r renders the 8x8
 blocks b % N == r and the shards are gathered to rank 0 INSIDE the timed region
-(frame_gather.FrameGather: rt_shard_pack, hipMemcpyAsync D2H into POSIX shared
-memory, one gloo barrier, H2D + rt_shard_unpack on rank 0) — the composite of
-src/renderer.rs:63-95. No collective touches the data path; gloo carries only the
+(frame_gather.FrameGather: every rank packs its blocks with rt_shard_pack, one gloo
+barrier, and rank 0 pulls the other ranks' packed shards straight out of their
+IPC-mapped device buffers over xGMI with rt_shard_pull_unpack; the /dev/shm bounce is
+the fallback where IPC is refused) — the composite of src/renderer.rs:63-95. No collective touches the data path; gloo carries only the
 barriers and the max over ranks of the timings. `--scaling weak` (opt-in) renders
 the full frame on every rank with disjoint sample ranges instead.
 
@@ -226,6 +227,10 @@ def main() -> int:
     total_samples = (samples_rank_launch * world if args.scaling == "weak" else W * H * spp) * args.steps
     img_ok = bool(torch.isfinite(frame[0]).all().item()) if frame[0] is not None else None
     frame_sum = float(frame[0].double().sum().item()) if rank == 0 and frame[0] is not None else None
+    frame_md5 = None
+    if rank == 0 and frame[0] is not None:  # position-sensitive: the frame's bytes, not a sum over them
+        import hashlib
+        frame_md5 = hashlib.md5(frame[0].cpu().numpy().tobytes()).hexdigest()
 
     if rank == 0:
         # BASELINE.json config 1 (C1) is the single-thread CPU reference over the whole frame
@@ -276,9 +281,9 @@ def main() -> int:
                        "scene": cfg.scene, "width": W, "height": H, "spp": spp, "max_depth": cfg.depth,
                        "parallelism": ("weak: full frame per GPU, disjoint sample ranges" if args.scaling == "weak"
                                        else f"strong: one fixed frame, 8x8 blocks b % {world} == rank per GPU, shards "
-                                            "gathered to rank 0 inside the timed region (rt_shard_pack, then "
-                                            "hipMemcpyAsync into rank 0's IPC-mapped buffer, or the /dev/shm bounce; "
-                                            "rt_shard_unpack; no collective)" if world > 1
+                                            "gathered to rank 0 inside the timed region (rt_shard_pack on every rank, "
+                                            "then rank 0 pulls the peers' IPC-mapped shards over xGMI with "
+                                            "rt_shard_pull_unpack, or the /dev/shm bounce; no collective)" if world > 1
                                        else "one GPU: the whole frame"),
                        "gather": gather.transport if gather is not None else None,
                        "exact_bvh": args.exact_bvh},
@@ -287,6 +292,7 @@ def main() -> int:
             "segments_per_sample": seg_total / total_samples if total_samples else None,
             "image_finite": img_ok,
             "frame_sum": frame_sum,
+            "frame_md5": frame_md5,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
                          "achieved_is": "SURVEY.md §8(d) algorithmic bytes per sample (the reference algorithm's "

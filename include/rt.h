@@ -376,19 +376,27 @@ int rt_shard_pack(const float* d_image, uint32_t width, uint32_t height, uint32_
 int rt_shard_unpack(const float* d_packed_all, uint32_t width, uint32_t height,
                     uint32_t n, float* d_image, void* stream);
 
-/* Peer transport for that gather (the north-star's hipMemcpyAsync gather to rank 0,
- * device to device over xGMI): rank 0 exports its gather buffer (rt_ipc_export: the
+/* Peer transport for that gather (device to device over xGMI, one hop), in pull form:
+ * every rank r > 0 exports its packed-shard buffer once (rt_ipc_export: the
  * hipIpcMemHandle_t of the allocation holding d_ptr plus d_ptr's offset in it, in
- * RT_IPC_HANDLE_BYTES bytes the caller sends to the other ranks), every other rank
- * maps it once (rt_ipc_open, on its own device; unmap with rt_ipc_close) and copies its
- * packed shard into its slot with rt_copy_async (a device-to-device hipMemcpyAsync on
- * `stream`). Replaces renderer.rs:86-95's host-side composite of the tiles; a /dev/shm
- * bounce stays the caller's fallback where IPC is refused. */
+ * RT_IPC_HANDLE_BYTES bytes the caller sends to rank 0) and rank 0 maps each of them
+ * (rt_ipc_open, on its own device; unmap with rt_ipc_close). Per frame each rank r > 0
+ * packs its blocks (rt_shard_pack, whose threads end with a system-scope release) and
+ * synchronises its stream; after a host barrier rank 0 calls rt_shard_pull_unpack with the
+ * n mapped pointers (entry 0 unused): one kernel, opening with a system-scope acquire
+ * fence, reads every peer word with a system-scope load and writes ranks 1..n-1's blocks
+ * into d_image, which already holds rank 0's own blocks. The visibility argument is the
+ * LLVM AMDGPU memory model's, not a dispatch default. Replaces
+ * renderer.rs:86-95's host-side composite of the tiles; a /dev/shm bounce stays the
+ * caller's fallback where IPC is refused. rt_copy_async is a device-to-device
+ * hipMemcpyAsync on `stream` (the transport's setup probe). At most 64 ranks. */
 #define RT_IPC_HANDLE_BYTES 72
 int rt_ipc_export(const void* d_ptr, int device, uint8_t handle[RT_IPC_HANDLE_BYTES]);
 int rt_ipc_open(const uint8_t handle[RT_IPC_HANDLE_BYTES], int device, void** d_ptr);
 int rt_ipc_close(void* d_ptr, int device);
 int rt_copy_async(void* d_dst, const void* d_src, uint64_t bytes, void* stream);
+int rt_shard_pull_unpack(const float* const* d_peer_packed, uint32_t width, uint32_t height,
+                         uint32_t n, float* d_image, void* stream);
 
 /* Scene builders restated from src/main.rs:185-829 ("random-spheres",
  * "random-moving-spheres", "two-spheres", "marble", "earth", "simple-lights",

@@ -128,6 +128,8 @@ SIGNATURES = [
     ("rt_ipc_open", C.c_int, [C.c_char_p, C.c_int, C.POINTER(C.c_void_p)]),
     ("rt_ipc_close", C.c_int, [C.c_void_p, C.c_int]),
     ("rt_copy_async", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]),
+    ("rt_shard_pull_unpack", C.c_int, [C.POINTER(C.c_void_p), C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p,
+                                       C.c_void_p]),
     ("rt_device_kat", C.c_int, [C.c_int, C.POINTER(C.c_float), C.POINTER(C.c_float), C.c_uint32]),
     ("rt_set_option", C.c_int, [C.c_int, C.c_int64]),
     ("rt_get_option", C.c_int, [C.c_int, C.POINTER(C.c_int64)]),

@@ -53,6 +53,40 @@ __global__ __launch_bounds__(256) void shard_pack(const float* __restrict__ img,
         dst[1] = src[1];
         dst[2] = src[2];
     }
+    // System-scope release: this thread's stores are written back past the L2 before it ends,
+    // so a peer that reads the packed shard over xGMI after the host has seen this stream
+    // complete (rt_shard_pull_unpack) finds them in memory whatever release scope the
+    // runtime gives the dispatch's end.
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+}
+
+// Pull form of the gather: rank 0 scatters the blocks of ranks 1..n-1 straight from their
+// packed-shard buffers (peer memory mapped with rt_ipc_open, read over xGMI) into its image;
+// its own blocks are already there. thread = (frame block b with b % n != 0, pixel slot p).
+constexpr uint32_t kMaxPullRanks = 64;
+struct PeerShards {
+    const float* p[kMaxPullRanks];  // p[r]: rank r's packed shard (k-th block of the rank at k * 64 slots)
+};
+__global__ __launch_bounds__(256) void shard_pull_unpack(PeerShards peers, uint32_t w, uint32_t h, uint32_t bx,
+                                                         uint32_t nb, uint32_t n, float* __restrict__ img) {
+    // System-scope acquire: the L1 / L2 lines a previous step left are invalidated before any
+    // peer word is read (with the writer's release in shard_pack and the host barrier between
+    // the writer's stream completion and this launch, the LLVM AMDGPU memory model makes every
+    // packed word visible here), and each peer word is read with a system-scope load.
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    const uint64_t slots = (uint64_t)nb * 64u;
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < slots; i += (uint64_t)gridDim.x * 256u) {
+        const uint32_t b = (uint32_t)(i >> 6), p = (uint32_t)(i & 63u);
+        const uint32_t r = b % n;
+        if (r == 0u) continue;
+        const uint32_t x = (b % bx) * 8u + (p & 7u), y = (b / bx) * 8u + (p >> 3);
+        if (x >= w || y >= h) continue;
+        const float* src = peers.p[r] + ((uint64_t)(b / n) * 64u + p) * 3u;
+        float* dst = img + ((uint64_t)y * w + x) * 3u;
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+            dst[c] = __hip_atomic_load(src + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 // thread = (frame block b, pixel slot p); shard b % n holds it at slot b / n
@@ -124,6 +158,27 @@ int rt_shard_unpack(const float* d_packed_all, uint32_t width, uint32_t height, 
                        d_packed_all, width, height, g.bx, g.nb, n, d_image);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? RT_OK : hip_fail(e, "shard_unpack launch");
+}
+
+int rt_shard_pull_unpack(const float* const* d_peer_packed, uint32_t width, uint32_t height, uint32_t n,
+                         float* d_image, void* stream) {
+    rthost::clear_error();
+    if (!d_peer_packed || !d_image || n == 0 || width == 0 || height == 0)
+        return rthost::set_error(RT_ERR_INVALID, "rt_shard_pull_unpack: NULL buffer, empty image or n == 0");
+    if (n > kMaxPullRanks) return rthost::set_error(RT_ERR_INVALID, "rt_shard_pull_unpack: more than 64 ranks");
+    if (n == 1) return RT_OK;
+    const Grid g = grid_of(width, height);
+    PeerShards peers{};
+    for (uint32_t r = 1; r < n; ++r) {
+        if (blocks_of(g.nb, r, n) && !d_peer_packed[r])
+            return rthost::set_error(RT_ERR_INVALID, "rt_shard_pull_unpack: NULL peer buffer");
+        peers.p[r] = d_peer_packed[r];
+    }
+    (void)hipGetLastError();
+    hipLaunchKernelGGL(shard_pull_unpack, dim3(launch_blocks((uint64_t)g.nb * 64u)), dim3(256), 0,
+                       (hipStream_t)stream, peers, width, height, g.bx, g.nb, n, d_image);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? RT_OK : hip_fail(e, "shard_pull_unpack launch");
 }
 
 // Peer transport (frame_gather.FrameGather's "ipc" path): rank 0 exports its gather

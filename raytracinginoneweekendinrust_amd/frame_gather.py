@@ -2,31 +2,34 @@
 
 The reference renders its tiles on a rayon pool and composites them into one
 image (src/renderer.rs:63-95). Here every rank is a process with its own GPU:
-rank r renders the 8x8 blocks b with b % n == r (rt_render_params.shard_index /
-shard_count) into a full-frame device image, and the frame is gathered to rank 0
+rank r of n renders the 8x8 blocks b with b % n == r (rt_render_params.shard_index /
+shard_count) into a full-frame device image, and the frame is assembled on rank 0
 without any collective on the data path:
 
-1. rank r packs its blocks into a dense device buffer (rt_shard_pack); rank 0
-   packs its own blocks straight into its gather buffer on the device;
-2. transport, one of
-   * "ipc" (default on GPUs): rank 0's gather buffer is exported once with
-     hipIpcGetMemHandle (rt_ipc_export) and mapped by every other rank
-     (rt_ipc_open); a rank copies its packed shard straight into its slot with one
-     device-to-device hipMemcpyAsync (rt_copy_async) — over xGMI between GPUs, the
-     north-star's "hipMemcpyAsync gather to rank 0", one hop;
-   * "shm" (fallback, and the CPU tests): one hipMemcpyAsync D2H into the rank's
-     slot of a POSIX shared-memory buffer (/dev/shm, page-locked with
-     hipHostRegister when the runtime allows it), then rank 0 copies the other
-     ranks' slots H2D;
-3. one gloo barrier ("every shard has landed"); rank 0 scatters all shards into
-   the final image (rt_shard_unpack).
+1. every rank r > 0 packs its blocks into a dense device buffer (rt_shard_pack,
+   whose threads end with a system-scope release) and synchronises its stream;
+2. one gloo barrier ("every shard is packed");
+3. transport, one of
+   * "ipc" (default on GPUs), a PULL over xGMI: every rank r > 0 exported its
+     two-slot packed-shard buffer once (rt_ipc_export) and rank 0 mapped them all
+     (rt_ipc_open); rank 0 starts from its own rendered image (its blocks) and one
+     kernel, rt_shard_pull_unpack, reads every other rank's blocks straight out of
+     the peers' memory (system-scope acquire fence, then system-scope loads) into
+     it — one hop, no intermediate copy, and the visibility of the peers' words
+     rests on the LLVM AMDGPU memory model (release by the writer's threads, host
+     barrier, acquire by the reader's), not on a dispatch default (DESIGN.md §7);
+   * "shm" (fallback, and the CPU tests): one hipMemcpyAsync D2H of the packed shard
+     into the rank's slot of a POSIX shared-memory buffer (/dev/shm, page-locked
+     with hipHostRegister when the runtime allows it, rank 0 packing its own shard
+     into the same layout), then rank 0 copies the other slots H2D and scatters all
+     shards (rt_shard_unpack).
 
-The gather buffer has two slots used in alternate steps, and rank 0 waits for its
-previous unpack before it enters a step's barrier: a rank writes slot s of step k+2
-only after the barrier of step k+1, by when rank 0's unpack of step k (the last
-reader of slot s) has completed, so a fast rank can never overwrite a shard rank 0
-is still reading. Pure copies, so the assembled frame is the
-one-device frame bit for bit.
+Slots alternate between steps, and rank 0 waits for its previous step's assembly
+before it enters a step's barrier: a rank writes slot s of step k+2 only after the
+barrier of step k+1, by when rank 0's read of step k (the last reader of slot s)
+has completed, so a fast rank can never overwrite a shard rank 0 is still reading
+(ADVICE r02). Pure copies, so the assembled frame is the one-device frame bit for
+bit (tests/test_gpu_multiprocess.py compares whole frames, step by step).
 """
 from __future__ import annotations
 
@@ -48,7 +51,7 @@ class FrameGather:
     `pack(d_image, w, h, rank, n, d_packed, stream)` / `unpack(d_all, w, h, n, d_image, stream)`
     default to the HIP kernels (rt_shard_pack / rt_shard_unpack); `device` is the torch
     device of this rank's buffers. Collective calls go to `group` (a gloo group).
-    `transport`: "auto" (ipc on GPUs when every rank can map rank 0's buffer, else shm),
+    `transport`: "auto" (ipc on GPUs when rank 0 can map and read every rank's buffer, else shm),
     "ipc" or "shm"; the one in use is `self.transport`."""
 
     def __init__(self, width: int, height: int, rank: int, world: int, device, group=None,
@@ -69,67 +72,83 @@ class FrameGather:
         self.step = 0
         self._unpacked = None  # rank 0: event recorded after the last unpack
         self._map = None
-        self._peer = None      # ranks > 0, ipc: rank 0's gather buffer mapped here
         self.host = None
         self.pinned = False
         cuda = self.device.type == "cuda"
+        self._peers = []       # rank 0, ipc: every rank's mapped two-slot packed buffer (entry 0 unused)
+        self._peer_cnt = []    # rank 0, ipc: floats per slot of each rank's buffer
         if rank == 0:
-            self.d_all = torch.empty(SLOTS * max(self.total, 1), dtype=torch.float32, device=self.device)
             self.image = torch.zeros(width * height * 3, dtype=torch.float32, device=self.device)
-        else:
-            self.d_pack = torch.empty(max(self.cnt, 1), dtype=torch.float32, device=self.device)
+        else:  # two slots of this rank's packed shard (alternate steps)
+            self.d_pack = torch.empty(SLOTS * max(self.cnt, 1), dtype=torch.float32, device=self.device)
         self.transport = "shm"
         if world > 1 and cuda and transport in ("auto", "ipc"):
             self.transport = self._open_ipc(transport == "ipc")
         if world > 1 and self.transport == "shm":
+            if rank == 0:
+                self.d_all = torch.empty(SLOTS * max(self.total, 1), dtype=torch.float32, device=self.device)
             self._open_shm()
 
     # --- transports ------------------------------------------------------------
     def _open_ipc(self, required: bool) -> str:
-        """Rank 0 exports its gather buffer, the others map it; every rank must succeed
-        (a MIN over the gloo group), else all fall back to shm together."""
+        """Every rank r > 0 exports its packed buffer, rank 0 maps them all and reads back a
+        probe word each rank wrote (r + 0.5 at slot 0): a transport that maps but delivers
+        nothing, or stale data, is caught here. Every rank must succeed (a MIN over the gloo
+        group), else all fall back to shm together."""
         import torch
         import torch.distributed as dist
-        from . import ipc_export, ipc_open
-        dev = self.device.index if self.device.index is not None else torch.cuda.current_device()
-        handle = [None]
+        from . import copy_async, ipc_export, ipc_open
+        dev = self._dev()
         ok = 1
+        handle = None
+        if self.rank != 0:
+            try:
+                self.d_pack[0].fill_(self.rank + 0.5)
+                self._sync()
+                handle = ipc_export(self.d_pack.data_ptr(), dev)
+            except Exception:
+                ok = 0
+        handles = [None] * self.world
+        dist.all_gather_object(handles, handle, group=self.group)
         if self.rank == 0:
+            probe = torch.zeros(self.world, dtype=torch.float32, device=self.device)
+            self._peers, self._peer_cnt = [0], [0]
             try:
-                handle[0] = ipc_export(self.d_all.data_ptr(), dev)
+                for r in range(1, self.world):
+                    cnt = shard_floats(self.w, self.h, r, self.world)
+                    if handles[r] is None:
+                        raise RuntimeError(f"rank {r} exported no buffer")
+                    ptr = ipc_open(handles[r], dev)
+                    self._peers.append(ptr)
+                    self._peer_cnt.append(max(cnt, 1))
+                    copy_async(probe.data_ptr() + 4 * r, ptr, 4, self._stream())
+                self._sync()
+                got = probe.cpu().tolist()
+                if any(got[r] != r + 0.5 for r in range(1, self.world)):
+                    raise RuntimeError(f"IPC probe read {got}")
             except Exception:
                 ok = 0
-        dist.broadcast_object_list(handle, src=0, group=self.group)
-        if self.rank != 0 and handle[0] is not None:
-            try:
-                self._peer = ipc_open(handle[0], dev)
-                if self.cnt:  # one real peer copy into this rank's slot, so a transport that maps but
-                    from . import copy_async  # cannot copy falls back here, not inside a timed step
-                    copy_async(self._peer + self.off * 4, self.d_pack.data_ptr(), 4, self._stream())
-                    self._sync()
-            except Exception:
-                ok = 0
-        elif handle[0] is None:
-            ok = 0
         flag = torch.tensor([ok], dtype=torch.int32)
         dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.group)
         if int(flag.item()) == 1:
             return "ipc"
-        if self._peer is not None:
-            self._close_ipc()
+        self._close_ipc()
         if required:
             raise RuntimeError("FrameGather: IPC transport unavailable on some rank")
         return "shm"
 
-    def _close_ipc(self):
+    def _dev(self) -> int:
         import torch
+        return self.device.index if self.device.index is not None else torch.cuda.current_device()
+
+    def _close_ipc(self):
         from . import ipc_close
-        dev = self.device.index if self.device.index is not None else torch.cuda.current_device()
-        try:
-            ipc_close(self._peer, dev)
-        except Exception:
-            pass
-        self._peer = None
+        for ptr in self._peers[1:]:
+            try:
+                ipc_close(ptr, self._dev())
+            except Exception:
+                pass
+        self._peers, self._peer_cnt = [], []
 
     def _open_shm(self):
         import torch
@@ -172,29 +191,37 @@ class FrameGather:
         st = self._stream()
         if self.world == 1:
             return d_image if self.rank == 0 else None
-        base = (self.step % SLOTS) * self.total
+        slot = self.step % SLOTS
         self.step += 1
         if self.rank == 0:
-            self._pack(d_image, self.w, self.h, 0, self.world, self.d_all[base: base + self.off1], st)
-            if self._unpacked is not None:  # the unpack of the previous step (last reader of the other slot)
+            if self._unpacked is not None:  # the previous step's assembly (last reader of the other slot)
                 self._unpacked.synchronize()
-        else:
-            if self.cnt:
-                self._pack(d_image, self.w, self.h, self.rank, self.world, self.d_pack[: self.cnt], st)
-                if self.transport == "ipc":
-                    from . import copy_async
-                    copy_async(self._peer + (base + self.off) * 4, self.d_pack.data_ptr(), self.cnt * 4, st)
-                else:
-                    self.host[base + self.off: base + self.off + self.cnt].copy_(self.d_pack[: self.cnt],
-                                                                                 non_blocking=self.pinned)
-            self._sync()
-        dist.barrier(group=self.group)  # every rank's shard is in rank 0's slot
+            if self.transport == "ipc":
+                self.image.copy_(d_image)  # rank 0's own blocks; the others are pulled below
+            else:
+                base = slot * self.total
+                self._pack(d_image, self.w, self.h, 0, self.world, self.d_all[base: base + self.off1], st)
+        elif self.cnt:
+            packed = self.d_pack[slot * self.cnt: (slot + 1) * self.cnt]
+            self._pack(d_image, self.w, self.h, self.rank, self.world, packed, st)
+            if self.transport == "shm":
+                base = slot * self.total
+                self.host[base + self.off: base + self.off + self.cnt].copy_(packed, non_blocking=self.pinned)
+        if self.rank != 0:
+            self._sync()  # the shard is packed (ipc) or in the shared slot (shm)
+        dist.barrier(group=self.group)  # every rank's shard is ready for rank 0
         if self.rank != 0:
             return None
-        if self.transport == "shm" and self.total > self.off1:
-            self.d_all[base + self.off1: base + self.total].copy_(self.host[base + self.off1: base + self.total],
-                                                                  non_blocking=self.pinned)
-        self._unpack(self.d_all[base: base + self.total], self.w, self.h, self.world, self.image, st)
+        if self.transport == "ipc":
+            from . import shard_pull_unpack
+            ptrs = [0] + [self._peers[r] + slot * self._peer_cnt[r] * 4 for r in range(1, self.world)]
+            shard_pull_unpack(ptrs, self.w, self.h, self.image, st)
+        else:
+            base = slot * self.total
+            if self.total > self.off1:
+                self.d_all[base + self.off1: base + self.total].copy_(self.host[base + self.off1: base + self.total],
+                                                                      non_blocking=self.pinned)
+            self._unpack(self.d_all[base: base + self.total], self.w, self.h, self.world, self.image, st)
         if self.device.type == "cuda":
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream(self.device))
@@ -203,7 +230,7 @@ class FrameGather:
 
     def close(self):
         import torch
-        if self._peer is not None:
+        if self._peers:
             self._close_ipc()
         if self._map is None:
             return

@@ -1,10 +1,13 @@
 """bench.py's N>1 path on the device, end to end: two processes (torch.distributed.run,
 gloo barriers), each rendering its 8x8 blocks b % 2 == rank with the HIP kernel, and the
-shared-memory gather of rt_shard_pack'ed shards to rank 0 (frame_gather.FrameGather).
-On a one-GPU box both ranks share the GPU (bench.py maps LOCAL_RANK onto the GPUs there).
-Rank 0's gathered frame must be the one-process frame bit for bit: its frame_sum (the f64
-sum of every float of the image) is compared exactly, and both lines must cover the same
-W*H*spp samples."""
+gather of rt_shard_pack'ed shards to rank 0 (frame_gather.FrameGather: the IPC pull over
+rt_shard_pull_unpack, or the /dev/shm bounce). On a one-GPU box the ranks share the GPU
+(bench.py maps LOCAL_RANK onto the GPUs there). Rank 0's gathered frame must be the
+one-process frame bit for bit: the md5 of its bytes is compared (position-sensitive: a
+swapped block or rank changes it; the f64 frame_sum would not notice). The FrameGather
+itself is also driven directly with a different, position-coded frame every step
+(tests/gather_worker.py), so both alternating slots are reused and a stale or misplaced
+word fails the step it lands in."""
 import json
 import os
 import socket
@@ -42,7 +45,7 @@ def test_two_rank_bench_gathers_the_one_gpu_frame():
                  (sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                   "--master-addr", "127.0.0.1", "--master-port", str(_port())))
     assert two["n_gpus"] == 2 and two["scaling"] == "strong"
-    assert two["frame_sum"] == one["frame_sum"]
+    assert two["frame_md5"] == one["frame_md5"]
     assert two["image_finite"] and one["image_finite"]
     assert two["rays_per_s"] > 0
     assert two["config"]["gather"] in ("ipc", "shm")
@@ -59,4 +62,22 @@ def test_two_rank_bench_back_to_back_frames_over_both_transports():
                      (sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                       "--master-addr", "127.0.0.1", "--master-port", str(_port())))
         assert two["config"]["gather"] == transport
-        assert two["frame_sum"] == one["frame_sum"], transport
+        assert two["frame_md5"] == one["frame_md5"], transport
+
+
+@pytest.mark.parametrize("transport,world", [("ipc", 2), ("ipc", 3), ("shm", 2)])
+def test_frame_gather_position_coded_frames(transport, world, tmp_path):
+    """FrameGather driven directly: 5 steps (both slots reused twice), a ragged 203 x 117
+    frame whose every float is distinct and changes each step; rank 0's frame must equal
+    it bit for bit after every step (tests/gather_worker.py)."""
+    out = tmp_path / "gather.json"
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
+                        "--master-addr", "127.0.0.1", "--master-port", str(_port()),
+                        os.path.join(ROOT, "tests", "gather_worker.py"), transport, "203", "117", "5", str(out)],
+                       capture_output=True, text=True, env=env, timeout=240, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = json.loads(out.read_text())
+    assert res["transport"] == transport and res["world"] == world
+    assert len(res["steps"]) == 5
+    assert all(st["equal"] for st in res["steps"]), res["steps"]

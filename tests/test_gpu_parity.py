@@ -322,11 +322,13 @@ def test_pruned_traversal_equals_reference_traversal_full_frame(cfg_name, spp, r
     assert out[True][1]["segments"] == out[False][1]["segments"]
 
 
-@pytest.mark.parametrize("cfg_name,spp", [("C3", 500), ("C4", 100)])
+@pytest.mark.parametrize("cfg_name,spp", [("C1", 50), ("C3", 500), ("C4", 100)])
 def test_traversal_audit_full_frame(cfg_name, spp):
-    # The audit build replays EVERY fast BVH traversal of a full C3 frame (500 spp) and of
-    # a full-resolution C4 frame (the suspending walk over the triangle BVH) with the
-    # literal bvh.rs recursion and re-tests every leaf-box reject; both counts must be 0.
+    # The audit build replays EVERY fast BVH traversal of a full C1 frame, a full C3 frame
+    # (500 spp) and a full-resolution C4 frame (the suspending walk over the triangle BVH)
+    # with the literal bvh.rs recursion and re-tests every leaf-box reject; both counts
+    # must be 0. The bounds count also covers take_sample's invariant that the whole wave
+    # is active where lane 0 claims a batch (kernel.hip take_sample).
     # Per-call (t, primitive) equality is stricter than the image tests: a tie resolved
     # to the wrong coplanar face can shade identically.
     import subprocess
