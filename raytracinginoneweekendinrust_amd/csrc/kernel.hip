@@ -1208,11 +1208,6 @@ RT_DEV bool bvh_run(const DevScene& S, float delta, const f4* wrapper, const Ray
         }
         PROF_ADD(kPrBvhTrip, pt);
         PROF_T0(pp);
-        sort2(t0, c0, t1, c1);
-        sort2(t2, c2, t3, c3);
-        sort2(t0, c0, t2, c2);
-        sort2(t1, c1, t3, c3);
-        sort2(t1, c1, t2, c2);
         // LDS stack; with kFDeep the entries past stack_depth go to the HBM spill area
         auto push = [&](uint32_t node, float t) {
             if (!(kF & kFDeep) || sp < S.stack_depth) {
@@ -1226,6 +1221,73 @@ RT_DEV bool bvh_run(const DevScene& S, float delta, const f4* wrapper, const Ray
             }
             sp += 1u;
         };
+#ifdef RT_MASKSTACK
+        if constexpr ((kF & kFTri) != 0u) {
+            if (!prune) {
+                // Per-level child-mask stack for an unprunable BVH (its visit set does not depend on
+                // the visit order): the first visited child is taken now and ONE entry,
+                // (this node, mask of its other visited children), is pushed; a pop takes the mask's
+                // lowest child from the node's child row. At most one entry per BVH4 level, so the
+                // stack stays in LDS (no HBM slab), with no sort and no entry distances.
+                auto rd = [&](uint32_t i) -> uint32_t {
+                    if (!(kF & kFDeep) || i < S.stack_depth) return stk[i * 128u];
+                    return S.stack_spill[(((size_t)blockIdx.x * S.spill_depth + (i - S.stack_depth)) * 64u + threadIdx.x) * 2u];
+                };
+                auto wr = [&](uint32_t i, uint32_t v) {
+                    if (!(kF & kFDeep) || i < S.stack_depth) stk[i * 128u] = v;
+                    else S.stack_spill[(((size_t)blockIdx.x * S.spill_depth + (i - S.stack_depth)) * 64u + threadIdx.x) * 2u] = v;
+                };
+                const uint32_t m = (t0 != kInf ? 1u : 0u) | (t1 != kInf ? 2u : 0u) | (t2 != kInf ? 4u : 0u) |
+                                   (t3 != kInf ? 8u : 0u);
+                if (m) {
+                    const uint32_t j = (uint32_t)__builtin_ctz(m), rest = m & (m - 1u);
+                    if (rest) {
+                        wr(sp, ((cur & ~rtdev::kLeafNodeFlag) << 4) | rest);
+                        sp += 1u;
+                    }
+                    cur = j == 0u ? c0 : (j == 1u ? c1 : (j == 2u ? c2 : c3));
+                    PROF_ADD(kPrBvhPush, pp);
+                    continue;
+                }
+                if (sp == 0u) break;
+                const uint32_t e = rd(sp - 1u), em = e & 15u, rest = em & (em - 1u);
+                const uint32_t j = (uint32_t)__builtin_ctz(em);
+                if (rest) wr(sp - 1u, (e & ~15u) | rest);
+                else sp -= 1u;
+                const f4 ch = ld4_at(S.nodes, (e >> 4) * (rtdev::kBvhNodeF4 * 16u) + 96u);
+                cur = __float_as_uint(j == 0u ? ch.x : (j == 1u ? ch.y : (j == 2u ? ch.z : ch.w)));
+                PROF_ADD(kPrBvhPush, pp);
+                continue;
+            }
+        }
+#endif
+#ifdef RT_UNORDERED
+        if constexpr ((kF & kFTri) != 0u) {
+            if (!prune) {
+                // An unprunable BVH's visit set does not depend on the visit order (every child
+                // box gets the reference's test with the entry t_max; the leaf-node results and
+                // the (t, DFS rank) merge are order-free), so no sort: the first
+                // visited slot is taken now and the others pushed as they come.
+                const bool v0 = t0 != kInf, v1 = t1 != kInf, v2 = t2 != kInf, v3 = t3 != kInf;
+                if (v0 || v1 || v2 || v3) {
+                    const uint32_t first = v0 ? c0 : (v1 ? c1 : (v2 ? c2 : c3));
+                    if (v3 && (v0 || v1 || v2)) push(c3, t3);
+                    if (v2 && (v0 || v1)) push(c2, t2);
+                    if (v1 && v0) push(c1, t1);
+                    cur = first;
+                    PROF_ADD(kPrBvhPush, pp);
+                    continue;
+                }
+                t0 = kInf;  // nothing to visit here: pop
+            }
+        }
+        if ((kF & kFTri) == 0u || prune) {
+#endif
+        sort2(t0, c0, t1, c1);
+        sort2(t2, c2, t3, c3);
+        sort2(t0, c0, t2, c2);
+        sort2(t1, c1, t3, c3);
+        sort2(t1, c1, t2, c2);
         if (t0 != kInf) {  // visit the nearest now, push the others far to near
             if (t3 != kInf) push(c3, t3);
             if (t2 != kInf) push(c2, t2);
@@ -1234,6 +1296,9 @@ RT_DEV bool bvh_run(const DevScene& S, float delta, const f4* wrapper, const Ray
             PROF_ADD(kPrBvhPush, pp);
             continue;
         }
+#ifdef RT_UNORDERED
+        }
+#endif
         PROF_ADD(kPrBvhPush, pp);
         PROF_T0(ppop);
         bool found = false;
@@ -2161,6 +2226,7 @@ struct ReplayItem {
     uint32_t pixel, sample;
 };
 constexpr unsigned long long kReplayFree = ~0ull;
+constexpr size_t kCamOffset = 256;  // RT_CAMMEM: byte offset of the launch's DevCamera copy behind the counters
 RT_DEV void replay_publish(ReplayItem* list, uint32_t idx, uint32_t pixel, uint32_t sample) {
     __hip_atomic_store(reinterpret_cast<unsigned long long*>(list + idx),
                        (unsigned long long)pixel | ((unsigned long long)sample << 32), __ATOMIC_RELAXED,
@@ -2502,6 +2568,16 @@ __global__ __launch_bounds__(64, kWaves) void trace_samples(DevScene Sg, DevCame
     }
     const Key k{P.seed_lo, P.seed_hi};
     const uint32_t mode = P.tune;
+#ifdef RT_CAMMEM
+    // the camera read from the device copy behind the counters at each new sample (not kept in
+    // SGPRs across the loop); the by-value argument is the same values. Only the flat-list
+    // preset's translation unit (kernel_flat.hip) is built this way: measured on the same box,
+    // C5 124.3 vs 126.5 ms per 200-spp frame, while the BVH presets lose 1-1.3% with it (C2,
+    // C3, C4; profiles/r04/experiments/camera_in_memory_ab_*.log).
+    const DevCamera& Cs = *reinterpret_cast<const DevCamera*>(reinterpret_cast<const char*>(ctr) + kCamOffset);
+#else
+    const DevCamera& Cs = C;
+#endif
     // item source: the chunk's block batches, or (fixup) the replay list
     unsigned* counter = &ctr->batch;
     const ReplayItem* list = nullptr;
@@ -2553,7 +2629,7 @@ __global__ __launch_bounds__(64, kWaves) void trace_samples(DevScene Sg, DevCame
         w.pos = 0u;
         for (;;) {
             PROF_T0(pr);
-            if (take_sample(pool, !has, C, P, Q, k, counter, list, list_n, ctr, stream_grid, sbuf, lane, slot, take_sample_idx, L, T, depth, g,
+            if (take_sample(pool, !has, Cs, P, Q, k, counter, list, list_n, ctr, stream_grid, sbuf, lane, slot, take_sample_idx, L, T, depth, g,
                             ray)) {
                 has = true;
                 w.pos = 0u;
@@ -2591,7 +2667,7 @@ __global__ __launch_bounds__(64, kWaves) void trace_samples(DevScene Sg, DevCame
     } else
     for (;;) {
         PROF_T0(pr);
-        if (take_sample(pool, !has, C, P, Q, k, counter, list, list_n, ctr, stream_grid, sbuf, lane, slot, take_sample_idx, L, T, depth, g,
+        if (take_sample(pool, !has, Cs, P, Q, k, counter, list, list_n, ctr, stream_grid, sbuf, lane, slot, take_sample_idx, L, T, depth, g,
                         ray)) {
             has = true;
         }
@@ -3347,7 +3423,8 @@ int rt_render_launch_camera(rt_scene_handle s, const rt_camera* camera, const rt
         s->sbuf_bytes = need;
     }
     if (!s->counter) {
-        if ((e = hipMalloc(&s->counter, sizeof(TraceCounters))) != hipSuccess)
+        static_assert(sizeof(TraceCounters) <= kCamOffset, "counters then the camera copy");
+        if ((e = hipMalloc(&s->counter, kCamOffset + sizeof(DevCamera))) != hipSuccess)
             return rthost::set_error(RT_ERR_OOM, std::string("hipMalloc counter: ") + hipGetErrorString(e));
     }
     if (!s->replay) {
@@ -3456,6 +3533,11 @@ int rt_render_launch_camera(rt_scene_handle s, const rt_camera* camera, const rt
         q.nslots = (uint32_t)nslots;
         if ((e = hipMemsetAsync(s->counter, 0, sizeof(TraceCounters), st)) != hipSuccess)
             return hip_fail(e, "memset counters");
+        // the launch's camera behind the counters: the flat-list instances (kernel_flat.hip, RT_CAMMEM)
+        // read it from there at each new sample instead of keeping 21 camera words in SGPRs
+        if (c == 0 && (e = hipMemcpyAsync(reinterpret_cast<char*>(s->counter) + kCamOffset, &cam, sizeof cam,
+                                          hipMemcpyHostToDevice, st)) != hipSuccess)
+            return hip_fail(e, "camera copy");
         uint32_t grid = (uint32_t)s->grid, grid_ref = (uint32_t)s->grid_ref;
         if (grid > q.units) grid = q.units;
         if (grid_ref > q.units) grid_ref = q.units;
