@@ -1221,68 +1221,6 @@ RT_DEV bool bvh_run(const DevScene& S, float delta, const f4* wrapper, const Ray
             }
             sp += 1u;
         };
-#ifdef RT_MASKSTACK
-        if constexpr ((kF & kFTri) != 0u) {
-            if (!prune) {
-                // Per-level child-mask stack for an unprunable BVH (its visit set does not depend on
-                // the visit order): the first visited child is taken now and ONE entry,
-                // (this node, mask of its other visited children), is pushed; a pop takes the mask's
-                // lowest child from the node's child row. At most one entry per BVH4 level, so the
-                // stack stays in LDS (no HBM slab), with no sort and no entry distances.
-                auto rd = [&](uint32_t i) -> uint32_t {
-                    if (!(kF & kFDeep) || i < S.stack_depth) return stk[i * 128u];
-                    return S.stack_spill[(((size_t)blockIdx.x * S.spill_depth + (i - S.stack_depth)) * 64u + threadIdx.x) * 2u];
-                };
-                auto wr = [&](uint32_t i, uint32_t v) {
-                    if (!(kF & kFDeep) || i < S.stack_depth) stk[i * 128u] = v;
-                    else S.stack_spill[(((size_t)blockIdx.x * S.spill_depth + (i - S.stack_depth)) * 64u + threadIdx.x) * 2u] = v;
-                };
-                const uint32_t m = (t0 != kInf ? 1u : 0u) | (t1 != kInf ? 2u : 0u) | (t2 != kInf ? 4u : 0u) |
-                                   (t3 != kInf ? 8u : 0u);
-                if (m) {
-                    const uint32_t j = (uint32_t)__builtin_ctz(m), rest = m & (m - 1u);
-                    if (rest) {
-                        wr(sp, ((cur & ~rtdev::kLeafNodeFlag) << 4) | rest);
-                        sp += 1u;
-                    }
-                    cur = j == 0u ? c0 : (j == 1u ? c1 : (j == 2u ? c2 : c3));
-                    PROF_ADD(kPrBvhPush, pp);
-                    continue;
-                }
-                if (sp == 0u) break;
-                const uint32_t e = rd(sp - 1u), em = e & 15u, rest = em & (em - 1u);
-                const uint32_t j = (uint32_t)__builtin_ctz(em);
-                if (rest) wr(sp - 1u, (e & ~15u) | rest);
-                else sp -= 1u;
-                const f4 ch = ld4_at(S.nodes, (e >> 4) * (rtdev::kBvhNodeF4 * 16u) + 96u);
-                cur = __float_as_uint(j == 0u ? ch.x : (j == 1u ? ch.y : (j == 2u ? ch.z : ch.w)));
-                PROF_ADD(kPrBvhPush, pp);
-                continue;
-            }
-        }
-#endif
-#ifdef RT_UNORDERED
-        if constexpr ((kF & kFTri) != 0u) {
-            if (!prune) {
-                // An unprunable BVH's visit set does not depend on the visit order (every child
-                // box gets the reference's test with the entry t_max; the leaf-node results and
-                // the (t, DFS rank) merge are order-free), so no sort: the first
-                // visited slot is taken now and the others pushed as they come.
-                const bool v0 = t0 != kInf, v1 = t1 != kInf, v2 = t2 != kInf, v3 = t3 != kInf;
-                if (v0 || v1 || v2 || v3) {
-                    const uint32_t first = v0 ? c0 : (v1 ? c1 : (v2 ? c2 : c3));
-                    if (v3 && (v0 || v1 || v2)) push(c3, t3);
-                    if (v2 && (v0 || v1)) push(c2, t2);
-                    if (v1 && v0) push(c1, t1);
-                    cur = first;
-                    PROF_ADD(kPrBvhPush, pp);
-                    continue;
-                }
-                t0 = kInf;  // nothing to visit here: pop
-            }
-        }
-        if ((kF & kFTri) == 0u || prune) {
-#endif
         sort2(t0, c0, t1, c1);
         sort2(t2, c2, t3, c3);
         sort2(t0, c0, t2, c2);
@@ -1296,9 +1234,6 @@ RT_DEV bool bvh_run(const DevScene& S, float delta, const f4* wrapper, const Ray
             PROF_ADD(kPrBvhPush, pp);
             continue;
         }
-#ifdef RT_UNORDERED
-        }
-#endif
         PROF_ADD(kPrBvhPush, pp);
         PROF_T0(ppop);
         bool found = false;
