@@ -339,9 +339,16 @@ RT_DEV Roots sphere_roots(f4 s, const RayD& q) {
     double disc = half_b * half_b - q.a * c;
     Roots R;
     R.ok = !sign_negative_d(disc);
-    double sq = __builtin_sqrt(disc);
-    R.r1 = (-half_b - sq) / q.a;
-    R.r2 = (-half_b + sq) / q.a;
+    R.r1 = R.r2 = 0.0;
+#ifdef RT_ROOTS_EARLY_OUT
+    if (R.ok) {  // a missed boundary (disc.is_sign_negative(), sphere.rs:69) needs neither root
+#endif
+        double sq = __builtin_sqrt(disc);
+        R.r1 = (-half_b - sq) / q.a;
+        R.r2 = (-half_b + sq) / q.a;
+#ifdef RT_ROOTS_EARLY_OUT
+    }
+#endif
     return R;
 }
 // sphere.rs:83-89 — near root unless outside [t_min, t_max], then the far root.
