@@ -68,7 +68,7 @@ def cpu_threads() -> int:
     return max(1, n)
 
 
-PMC_DIRS = (os.path.join(ROOT, "profiles", "r03"), os.path.join(ROOT, "profiles"))
+PMC_DIRS = (os.path.join(ROOT, "profiles", "r04"), os.path.join(ROOT, "profiles", "r03"), os.path.join(ROOT, "profiles"))
 
 
 def library_md5() -> str:

@@ -439,34 +439,9 @@ RT_DEV void rect_axes(uint32_t axis, const Ray& r, float& ok, float& dk, float& 
 }
 // rectangle.rs:36-65 with the plane axis resolved: k along (ok, dk), bounds
 // [a0, a1] x [b0, b1] along (oa, da) x (ob, db). Same IEEE operations as rect_t.
-// Division-free rejects for rectangle.rs:36-65's t = (k - o) / d: true only when the reference's
-// correctly rounded quotient certainly fails `t < t_min || t > t_max`, so the rectangle is
-// rejected without the division (a correctly rounded f32 division is ~10 VALU instructions).
-// Exact cases only, and only for t_min > 0 (the world walk's 0.001; a medium's boundary.hit
-// passes -inf): a zero numerator or numerator and denominator of opposite signs give a
-// quotient <= 0 < t_min; and with p = |d| * t_max (f32, >= 2^-100 so that no underflow hides
-// the rounding), |k - o| > p * (1 + 2^-20) means |q| > t_max (1 + 2^-20)(1 - 2^-24)^2 >
-// t_max (1 + 2^-21), so the rounded quotient exceeds t_max. A zero, non-finite or NaN
-// operand is left to the division (0 / 0 is the reference's NaN hit).
-RT_DEV bool rect_surely_rejected(float num, float dk, float tmin, float tmax) {
-#ifdef RT_RECT_DIVFREE
-    if (!(tmin > 0.0f)) return false;
-    const float an = __builtin_fabsf(num), ad = __builtin_fabsf(dk);
-    if (!(ad > 0.0f) || !(ad < kInf) || !(an < kInf)) return false;
-    if (an == 0.0f || ((__float_as_uint(num) ^ __float_as_uint(dk)) >> 31) != 0u) return true;
-    const float p = ad * tmax;
-    return p >= 0x1p-100f && an > p * (1.0f + 0x1p-20f);
-#else
-    return false;
-#endif
-}
 RT_DEV bool side_t(float k, float ok, float dk, float oa, float da, float ob, float db, float a0, float a1, float b0,
                    float b1, float tmin, float tmax, float& t) {
-    const float num = k - ok;
-#if defined(RT_RECT_DIVFREE) && RT_RECT_DIVFREE >= 2
-    if (rect_surely_rejected(num, dk, tmin, tmax)) return false;
-#endif
-    const float tt = num / dk;
+    const float tt = (k - ok) / dk;
     if (tt < tmin || tt > tmax) return false;
     const float x = oa + tt * da;
     const float y = ob + tt * db;
@@ -477,9 +452,7 @@ RT_DEV bool side_t(float k, float ok, float dk, float oa, float da, float ob, fl
 RT_DEV bool rect_t(f4 r0, f4 r1, const Ray& r, float tmin, float tmax, float& t) {
     float ok, dk, oa, da, ob, db;
     rect_axes(__float_as_uint(r1.y), r, ok, dk, oa, da, ob, db);
-    const float num = r0.x - ok;
-    if (rect_surely_rejected(num, dk, tmin, tmax)) return false;
-    float tt = num / dk;
+    float tt = (r0.x - ok) / dk;
     if (tt < tmin || tt > tmax) return false;
     float x = oa + tt * da;
     float y = ob + tt * db;

@@ -4,10 +4,13 @@
 # 1. tools/profile.sh per config (rocprofv3 kernel trace + the PMC passes), 2. the PMC summaries
 # (tools/valu_roofline.py, written where bench.py reads them and copied under gpurun_out/), 3. one
 # bench line per config plus a driver-style C3 line, 4. the GPU suite and smoke(). Every GPU step
-# has its own time limit; the script stops at the first failure.
+# has its own time limit; the script stops at the first failure. gpurun allows 20 minutes per call,
+# so the session runs in two calls: `bash tools/final_evidence.sh profiles` (1-2), then
+# `bash tools/final_evidence.sh bench` (3-4); no argument runs both.
 set -u
+PHASE="${1:-all}"
 cd "$(dirname "$0")/.."
-OUT=gpurun_out/final
+OUT=gpurun_out/final4
 mkdir -p "$OUT/pmc"
 export TMPDIR=/tmp
 run() {  # run <log> <seconds> <cmd...>
@@ -22,15 +25,19 @@ run() {  # run <log> <seconds> <cmd...>
         exit $rc
     fi
 }
-for c in C3 C1 C2 C4 C5; do
-    run "profile_$c.log" 900 bash tools/profile.sh final "$c"
-    run "roofline_$c.log" 120 python3 tools/valu_roofline.py "gpurun_out/prof_final_$c" --out-dir profiles/r03
-    cp "profiles/r03/pmc_valu_$c.json" "profiles/r03/pmc_traffic_$c.json" "$OUT/pmc/"
-done
-for c in C3 C1 C2 C4 C5; do
-    run "bench_$c.log" 300 python3 -u bench.py --config "$c"
-done
-run bench_driver_style.log 300 python3 -u bench.py --gpus 1 --steps 20 --warmup 5
-run gpu_tests.log 900 python3 -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread
-run smoke.log 300 python3 -u -c "import __graft_entry__ as g; g.smoke()"
+if [ "$PHASE" != bench ]; then
+    for c in C3 C1 C2 C4 C5; do
+        run "profile_$c.log" 900 bash tools/profile.sh final4 "$c"
+        run "roofline_$c.log" 120 python3 tools/valu_roofline.py "gpurun_out/prof_final4_$c" --out-dir profiles/r04
+        cp "profiles/r04/pmc_valu_$c.json" "profiles/r04/pmc_traffic_$c.json" "$OUT/pmc/"
+    done
+fi
+if [ "$PHASE" != profiles ]; then
+    for c in C3 C1 C2 C4 C5; do
+        run "bench_$c.log" 300 python3 -u bench.py --config "$c"
+    done
+    run bench_driver_style.log 300 python3 -u bench.py --gpus 1 --steps 20 --warmup 5
+    run gpu_tests.log 900 python3 -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread
+    run smoke.log 300 python3 -u -c "import __graft_entry__ as g; g.smoke()"
+fi
 echo "== final evidence done" | tee -a "$OUT/session.log"
