@@ -129,6 +129,17 @@ def test_output_and_multi_entry_points_reject_bad_arguments(rt):
     p2 = rt.render_params(8, 8, 1, 1, shard_index=0, shard_count=2)
     assert lib.rt_render_multi(hs, 2, C.byref(cam), C.byref(p2), out.ctypes.data_as(C.POINTER(C.c_float)), None) == INVALID
     assert "shards" in rt.lib.rt_last_error().decode()
+    # the pull form of the gather: NULL arrays, more than 64 ranks and a NULL peer buffer of a
+    # rank that owns blocks are refused before any launch; one rank has nothing to pull
+    img = C.c_void_p(1)
+    peers = (C.c_void_p * 65)(*([None] + [1] * 64))
+    assert lib.rt_shard_pull_unpack(None, 16, 16, 2, img, None) == INVALID
+    assert lib.rt_shard_pull_unpack(peers, 16, 16, 65, img, None) == INVALID
+    assert "64 ranks" in rt.lib.rt_last_error().decode()
+    holes = (C.c_void_p * 2)(None, None)
+    assert lib.rt_shard_pull_unpack(holes, 16, 16, 2, img, None) == INVALID
+    assert "peer buffer" in rt.lib.rt_last_error().decode()
+    assert lib.rt_shard_pull_unpack(holes, 16, 16, 1, img, None) == 0
 
 
 def test_one_hip_runtime_per_process(rt):
