@@ -127,8 +127,9 @@ def reference(rt, orc, spp_mult=1):
     return img
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_strong_scaling_gather_assembles_the_frame(rt, orc, world):
+    # world 8: the bench's 8-GPU decomposition (20 blocks over 8 ranks: 3, 3, 3, 3, 2, 2, 2, 2)
     frames, wall = run("strong", world)
     np.testing.assert_array_equal(frames[0], reference(rt, orc))
     assert wall > 0
