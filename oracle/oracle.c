@@ -1314,12 +1314,23 @@ static V3 ray_color_rec(const OScene* s, const ORay* ray, uint32_t depth, V3 bg,
 /* The device's order: L += T*e at each vertex, T *= attenuation (forward
  * product). Same random draws and branches as the recursion; radiance differs
  * from it only by float reassociation (checked <= 1e-5 in tests). */
+#ifdef ORACLE_TRACE
+static __thread int g_trace; /* diagnostic build only: get_color sets it for one (pixel, sample) */
+static uint32_t fbits(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }
+#endif
 static V3 ray_color_fwd(const OScene* s, ORay ray, uint32_t depth, V3 bg, OCtx* c) {
     V3 L = v3(0.0f, 0.0f, 0.0f), T = v3(1.0f, 1.0f, 1.0f);
     while (depth > 0) {
         c->cnt->segments++;
         ORec rec;
-        if (!hittable_hit(s->world, &ray, 0.001f, INFINITY, c, &rec)) {
+        int hit = hittable_hit(s->world, &ray, 0.001f, INFINITY, c, &rec);
+#ifdef ORACLE_TRACE
+        if (g_trace)
+            fprintf(stderr, "TRACE depth %u o %08x %08x %08x d %08x %08x %08x any %d t %08x\n", depth, fbits(ray.o.x),
+                   fbits(ray.o.y), fbits(ray.o.z), fbits(ray.d.x), fbits(ray.d.y), fbits(ray.d.z), hit,
+                   hit ? fbits(rec.t) : 0x7f800000u);
+#endif
+        if (!hit) {
             L = vadd(L, vmul(T, bg));
             break;
         }
@@ -1461,6 +1472,9 @@ static V3 get_color(const OJob* j, uint32_t x, uint32_t y, OCtx* c) {
     uint32_t pixel = y * p->width + x;
     for (uint32_t s = 0; s < p->samples_per_pixel; ++s) {
         rng_init(&c->rng, p->seed, pixel, p->sample_base + s);
+#ifdef ORACLE_TRACE
+        g_trace = pixel == ORACLE_TRACE_PIXEL && p->sample_base + s == ORACLE_TRACE_SAMPLE;
+#endif
         c->cnt->samples++;
         float u = ((float)x + rng_std01(&c->rng)) / (float)(p->width - 1);
         float v = ((float)y + rng_std01(&c->rng)) / (float)(p->height - 1);

@@ -175,6 +175,30 @@ __device__ TravAudit g_trav_audit[kAuditMax];
 struct V {
     float x, y, z;
 };
+#ifdef RT_DEBUG_PIXEL
+// Diagnostic builds only: records of one (pixel, sample)'s path, read back after the render
+// (the host prints them to stderr). Plain stores, so the instrumented kernel stays close to the
+// product's code.
+constexpr uint32_t kDbgMax = 256;
+__device__ uint32_t g_dbg[8 * kDbgMax];
+__device__ unsigned g_dbg_n;
+#ifndef RT_DEBUG_TRACE
+#define RT_DEBUG_TRACE 1
+#endif
+#ifdef RT_DEBUG_INLINE
+__device__ __forceinline__
+#else
+__device__ __noinline__
+#endif
+void dbg_put(uint32_t tag, uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t e,
+                                     uint32_t f, uint32_t h) {
+    const unsigned i = atomicAdd(&g_dbg_n, 1u);
+    if (i < kDbgMax) {
+        uint32_t* o = g_dbg + 8u * i;
+        o[0] = tag; o[1] = a; o[2] = b; o[3] = c; o[4] = d; o[5] = e; o[6] = f; o[7] = h;
+    }
+}
+#endif
 RT_DEV V mk(float x, float y, float z) { return V{x, y, z}; }
 RT_DEV V operator+(V a, V b) { return V{a.x + b.x, a.y + b.y, a.z + b.z}; }
 RT_DEV V operator-(V a, V b) { return V{a.x - b.x, a.y - b.y, a.z - b.z}; }
@@ -267,7 +291,36 @@ uint4 philox_block(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t k0, uint32_t 
     philox(c0, c1, c2, c3, k0, k1);
     return make_uint4(c0, c1, c2, c3);
 }
+// RT_RNG_UNIFORM (the main translation unit, where philox_block is an out-of-line call): the
+// block is computed under a wave-uniform branch (any active lane needs one) and taken per
+// lane by select, so no divergent join carries the buffer. With the per-lane branch around
+// the call, ROCm 7.2's VGPR allocator split the buffer's live ranges at the top of the join,
+// ahead of its EXEC restore, so the copies moved r0 / r2 for the calling lanes only and the
+// others' next draw was wrong (the C1 / C4 builds that left the oracle's bits; DESIGN.md §5,
+// tools/exec_join_check.py, which tests/test_exec_join.py runs on every product build). The
+// wave runs the call whenever any lane needs it in either form; the selects cost C4 nothing
+// measurable. The inlined-Philox units keep the per-lane branch (no call, no such split
+// there; the uniform form measured C3 -1.8%, C5 -1.2%) and are covered by the same check.
+#ifndef RT_RNG_UNIFORM
+#ifdef RT_PHILOX_INLINE
+#define RT_RNG_UNIFORM 0
+#else
+#define RT_RNG_UNIFORM 1
+#endif
+#endif
 RT_DEV uint32_t next_u32(Rng& g, const Key& k) {
+#if RT_RNG_UNIFORM
+    const bool fresh = (g.d & 3u) == 0u;
+    uint32_t r = g.r0, r0 = g.r1, r1 = g.r2, r2 = g.r2;
+    if (__ballot(fresh) != 0ull) {
+        const uint4 b = philox_block(g.d >> 2, g.sample, g.pixel, k.k0, k.k1);
+        r = fresh ? b.x : r;
+        r0 = fresh ? b.y : r0;
+        r1 = fresh ? b.z : r1;
+        r2 = fresh ? b.w : r2;
+    }
+    g.r0 = r0; g.r1 = r1; g.r2 = r2;
+#else
     uint32_t r;
     if ((g.d & 3u) == 0u) {
         const uint4 b = philox_block(g.d >> 2, g.sample, g.pixel, k.k0, k.k1);
@@ -277,6 +330,7 @@ RT_DEV uint32_t next_u32(Rng& g, const Key& k) {
         r = g.r0;
         g.r0 = g.r1; g.r1 = g.r2;
     }
+#endif
     g.d += 1u;
     return r;
 }
@@ -1785,6 +1839,10 @@ RT_DEV bool scatter(const DevScene& S, const DevMaterial& m, const Ray& r, const
         PROF_T0(pu);
         rs = in_unit_sphere(g, k);
         PROF_ADD(kPrUnitSphere, pu);
+#ifdef RT_DEBUG_PIXEL
+        if ((RT_DEBUG_TRACE & 2) && g.pixel == RT_DEBUG_PIXEL && g.sample == RT_DEBUG_SAMPLE)
+            dbg_put(2u, __float_as_uint(rs.x), __float_as_uint(rs.y), __float_as_uint(rs.z), g.d, g.r0, g.r1, g.r2);
+#endif
     }
     if (m.kind == rtdev::kMatLambertian) {  // lambertian.rs:34-53
         PROF_T0(pb);
@@ -2348,6 +2406,12 @@ RT_DEV bool finish_segment(const DevScene& S, const DevParams& P, const ChunkPar
                            float* __restrict__ sbuf, bool any, uint32_t he, uint32_t hc, float t, Ray& ray, V& L, V& T,
                            uint32_t& depth, Rng& g, uint32_t slot, uint32_t s_local) {
     PROF_T0(pg);
+#ifdef RT_DEBUG_PIXEL
+    // diagnostic builds only (tools/trace_sample.py): RT_DEBUG_TRACE bit 1 records the segment's
+    // entry (Rng state and hit), bit 2 the in_unit_sphere draw, bit 4 the scatter's result
+    if ((RT_DEBUG_TRACE & 1) && g.pixel == RT_DEBUG_PIXEL && g.sample == RT_DEBUG_SAMPLE)
+        dbg_put(1u, depth, g.d, g.r0, g.r1, g.r2, any ? hc : 0xffffffffu, __float_as_uint(t));
+#endif
     bool done;
     if (!any) {
         L = L + T * mk(P.bg[0], P.bg[1], P.bg[2]);
@@ -2370,6 +2434,11 @@ RT_DEV bool finish_segment(const DevScene& S, const DevParams& P, const ChunkPar
         PROF_T0(ps);
         bool scattered = scatter(S, m, ray, rec, g, k, att, sc);
         PROF_ADD(kPrScatter, ps);
+#ifdef RT_DEBUG_PIXEL
+        if ((RT_DEBUG_TRACE & 4) && g.pixel == RT_DEBUG_PIXEL && g.sample == RT_DEBUG_SAMPLE)
+            dbg_put(3u, rec.mat, m.kind, __float_as_uint(sc.d.x), __float_as_uint(sc.d.y), __float_as_uint(sc.d.z), g.d,
+                    __float_as_uint(rec.n.y));
+#endif
         if (scattered) {
             T = T * att;
             ray = sc;
@@ -3159,6 +3228,17 @@ int rt_scene_free(rt_scene_handle s) {
                     fprintf(stderr, "%s%.3f", i ? "," : "", (double)tp[i] / (kTpTicks * 10.0));
                 fprintf(stderr, "]}}\n");
             }
+        }
+#endif
+#ifdef RT_DEBUG_PIXEL
+        {
+            unsigned nd = 0;
+            static uint32_t dv[8 * kDbgMax];
+            if (hipMemcpyFromSymbol(&nd, HIP_SYMBOL(g_dbg_n), sizeof nd) == hipSuccess &&
+                hipMemcpyFromSymbol(dv, HIP_SYMBOL(g_dbg), sizeof dv) == hipSuccess)
+                for (unsigned i = 0; i < nd && i < kDbgMax; ++i)
+                    fprintf(stderr, "DBG %u %08x %08x %08x %08x %08x %08x %08x\n", dv[8 * i], dv[8 * i + 1],
+                            dv[8 * i + 2], dv[8 * i + 3], dv[8 * i + 4], dv[8 * i + 5], dv[8 * i + 6], dv[8 * i + 7]);
         }
 #endif
 #ifdef RT_LEAF_AUDIT

@@ -32,6 +32,7 @@ def bind(spec, idx):
     copy = os.path.join(tempfile.gettempdir(), f"ab_{os.getpid()}_{idx}_{os.path.basename(path)}")
     shutil.copyfile(path, copy)
     lib = C.CDLL(copy)
+    os.unlink(copy)  # the mapping stays valid; nothing is left in the temp directory
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import rtopts
     rtopts.apply_lib(lib)
