@@ -1102,17 +1102,6 @@ RT_DEV bool bvh_run(const DevScene& S, float delta, const f4* wrapper, const Ray
     // the max plane is entered first when 1/d < 0); the far row is the other one (off ^ c).
     [[maybe_unused]] const uint32_t hnx = inv.x < 0.0f ? 48u : 0u, hny = inv.y < 0.0f ? 64u : 16u,
                                     hnz = inv.z < 0.0f ? 80u : 32u;
-#if defined(RT_EXP_PERTURB) && RT_EXP_PERTURB == 2
-    if (mode & (1u << 30)) {  // never: the wrapper's box tested again
-        float te;
-        const f4 a = ld4(wrapper), b = ld4(wrapper + 1);
-        if (!slab(a.x, a.y, a.z, a.w, b.x, b.y, r, inv, tmin, tv.tmax_entry, te)) {
-            tv.any = false;
-            tv.sp = 0u;
-            return true;
-        }
-    }
-#endif
     bool any = tv.any;
     uint32_t best_rank = tv.best_rank, sp = tv.sp, cur = tv.cur;
     bool finished = true;
@@ -1309,16 +1298,6 @@ RT_DEV bool bvh_run(const DevScene& S, float delta, const f4* wrapper, const Ray
                 found = true;
                 break;
             }
-#if defined(RT_EXP_PERTURB) && RT_EXP_PERTURB == 9
-            if (mode & (1u << 30)) {  // never: re-test the popped subtree's parent row
-                const f4 a = ld4(S.nodes + (size_t)(cand & ~rtdev::kLeafNodeFlag) * rtdev::kBvhNodeF4 + 6);
-                if (__float_as_uint(a.x) == cand) {
-                    cur = __float_as_uint(a.y);
-                    found = true;
-                    break;
-                }
-            }
-#endif
         }
         PROF_ADD(kPrBvhPop, ppop);
         if (!found) break;
@@ -1425,10 +1404,6 @@ RT_DEV bool entry_geom_hit(const DevScene& S, float delta, const DevEntry* E, Ra
             ABLATE(kAbBvh2, float c2 = closest; uint32_t h2 = 0u; bool rp = false;
                    if (bvh_hit<kKind, kF>(S, delta, E->payload, r, tmin, c2, h2, stk, mode, rp) && h2 == 0x7fffffffu)
                        closest = -1.0f;);
-#if defined(RT_EXP_PERTURB) && RT_EXP_PERTURB == 6
-            if (mode & (1u << 30))  // never: the literal recursion inside the fast kernel
-                return bvh_hit<1, kF>(S, delta, E->payload, r, tmin, closest, hit_code, stk, mode, replay);
-#endif
             return bvh_hit<kKind, kF>(S, delta, E->payload, r, tmin, closest, hit_code, stk, mode, replay);
         }
     }
@@ -1951,127 +1926,9 @@ RT_DEV bool world_hit(const DevScene& S, float delta, const Ray& r, Rng& g, cons
                       uint32_t& hit_entry, uint32_t& hit_code, uint32_t* stk, uint32_t mode, bool& replay) {
     float closest = kInf;
     bool any = false;
-    // Code-generation stability sweep (tools/perturb_sweep.sh): RT_EXP_DEAD and
-    // RT_EXP_PERTURB=1..10 compile never-executed blocks into the instances (gated by bit 30 of
-    // RT_OPT_TUNE, which nothing sets, or by a scene property no scene has); every such build
-    // must render the product's bits. Product builds define neither.
-#ifdef RT_EXP_DEAD
-    // a reconstruction of round 3's deferred-first-BVH walk (its source was not kept)
-    if ((mode & (1u << 30)) && S.num_top > 1u && S.entries[0].kind == rtdev::kEntBvh) {
-        bool plain = true;
-        for (uint32_t e = 1; e < S.num_top; ++e)
-            if (S.entries[e].kind == rtdev::kEntMedium) plain = false;
-        if (plain) {
-            for (uint32_t e = 1; e < S.num_top; ++e) {
-                uint32_t code;
-                if (entry_geom_hit<kKind, kF>(S, delta, S.entries + e, r, 0.001f, closest, code, stk, mode, replay)) {
-                    hit_entry = e;
-                    hit_code = code;
-                    any = true;
-                }
-            }
-            float c0 = closest;
-            uint32_t code0 = 0u;
-            if (entry_geom_hit<kKind, kF>(S, delta, S.entries, r, 0.001f, c0, code0, stk, mode, replay) &&
-                c0 < closest) {
-                closest = c0;
-                hit_entry = 0u;
-                hit_code = code0;
-                any = true;
-            }
-            t_hit = closest;
-            return any;
-        }
-    }
-#endif
-#if defined(RT_EXP_PERTURB) && (RT_EXP_PERTURB == 7 || RT_EXP_PERTURB == 8)
-    // never: the deferred first BVH with the reference's tie rules restated
-#if RT_EXP_PERTURB == 7
-    const bool defer = (mode & (1u << 30)) && S.num_top > 1u && S.entries[0].kind == rtdev::kEntBvh;
-#else
-    const bool defer = S.num_top > 1u && S.entries[0].kind == rtdev::kEntBvh && S.entries[S.num_top - 1u].ntf > 3u;
-#endif
-    if (defer) {
-        uint32_t stop = S.num_top;
-        for (uint32_t e = 1; e < S.num_top; ++e)
-            if (S.entries[e].kind == rtdev::kEntMedium) {
-                stop = e;
-                break;
-            }
-        float c1 = kInf;
-        uint32_t he1 = 0u, hc1 = 0u;
-        bool a1 = false;
-        for (uint32_t e = 1; e < stop; ++e) {
-            uint32_t code = 0u;
-            if (entry_geom_hit<kKind, kF>(S, delta, S.entries + e, r, 0.001f, c1, code, stk, mode, replay)) {
-                he1 = e;
-                hc1 = code;
-                a1 = true;
-            }
-        }
-        // the BVH with the others' bound, nudged up one ulp so an f64 root that rounds onto c1 is seen
-        float c0 = c1 < kInf ? __uint_as_float(__float_as_uint(c1) + 1u) : kInf;
-        uint32_t hc0 = 0u;
-        const bool a0 = entry_geom_hit<kKind, kF>(S, delta, S.entries, r, 0.001f, c0, hc0, stk, mode, replay);
-        if (a0 && (!a1 || c0 < c1 || c0 != c0)) {
-            closest = c0;
-            hit_entry = 0u;
-            hit_code = hc0;
-            any = true;
-        } else if (a1) {
-            closest = c1;
-            hit_entry = he1;
-            hit_code = hc1;
-            any = true;
-        }
-        for (uint32_t e = stop; e < S.num_top; ++e) {
-            const DevEntry* E = S.entries + e;
-            if (E->kind == rtdev::kEntMedium) {
-                float t;
-                if (medium_hit<kKind, kF>(S, delta, E, r, 0.001f, closest, g, k, t, stk, mode, replay)) {
-                    closest = t;
-                    hit_entry = e;
-                    hit_code = rtdev::leaf_code(rtdev::kLeafMedium, 0);
-                    any = true;
-                }
-            } else {
-                uint32_t code;
-                if (entry_geom_hit<kKind, kF>(S, delta, E, r, 0.001f, closest, code, stk, mode, replay)) {
-                    hit_entry = e;
-                    hit_code = code;
-                    any = true;
-                }
-            }
-        }
-        t_hit = closest;
-        return any;
-    }
-#endif
-#if defined(RT_EXP_PERTURB) && RT_EXP_PERTURB == 1
-    uint32_t deferred = 0xffffffffu;
-    auto flush = [&]() {
-        float c0 = closest;
-        uint32_t code0 = 0u;
-        if (entry_geom_hit<kKind, kF>(S, delta, S.entries + deferred, r, 0.001f, c0, code0, stk, mode, replay) &&
-            c0 < closest) {
-            closest = c0;
-            hit_entry = deferred;
-            hit_code = code0;
-            any = true;
-        }
-        deferred = 0xffffffffu;
-    };
-#endif
     for (uint32_t e = 0; e < S.num_top; ++e) {
         const DevEntry* E = S.entries + e;
         PROF_T0(pe);
-#if defined(RT_EXP_PERTURB) && RT_EXP_PERTURB == 1
-        if (e == 0u && (mode & (1u << 30)) && E->kind == rtdev::kEntBvh && S.num_top > 1u) {
-            deferred = e;
-            continue;
-        }
-        if (deferred != 0xffffffffu && E->kind == rtdev::kEntMedium) flush();
-#endif
         if (E->kind == rtdev::kEntMedium) {
             float t;
             if (medium_hit<kKind, kF>(S, delta, E, r, 0.001f, closest, g, k, t, stk, mode, replay)) {
@@ -2090,28 +1947,6 @@ RT_DEV bool world_hit(const DevScene& S, float delta, const Ray& r, Rng& g, cons
         }
         PROF_ADD(e < kPrEntryLast - kPrEntry0 ? kPrEntry0 + e : kPrEntryLast, pe);
     }
-#if defined(RT_EXP_PERTURB) && RT_EXP_PERTURB == 1
-    if (deferred != 0xffffffffu) flush();
-#endif
-#if defined(RT_EXP_PERTURB) && RT_EXP_PERTURB == 4
-    if ((mode & (1u << 30)) && any) {  // never: a second walk
-        float c2 = kInf;
-        uint32_t he2 = 0u, hc2 = 0u;
-        for (uint32_t e = 0; e < S.num_top; ++e) {
-            uint32_t code = 0u;
-            if (S.entries[e].kind != rtdev::kEntMedium &&
-                entry_geom_hit<kKind, kF>(S, delta, S.entries + e, r, 0.001f, c2, code, stk, mode, replay)) {
-                he2 = e;
-                hc2 = code;
-            }
-        }
-        if (c2 != closest) {
-            closest = c2;
-            hit_entry = he2;
-            hit_code = hc2;
-        }
-    }
-#endif
     t_hit = closest;
     return any;
 }
@@ -2325,10 +2160,6 @@ RT_DEV bool take_sample(ItemPool& pool, bool want, const DevCamera& C, const Dev
                     const uint32_t rem = cur < Q.units ? Q.units - cur : 0u;
                     cnt = rem / (Q.guide * gridDim.x);
                     cnt = cnt < 1u ? 1u : (cnt > Q.group ? Q.group : cnt);
-#if defined(RT_EXP_PERTURB) && RT_EXP_PERTURB == 3
-                    if (P.tune & (1u << 30))  // never
-                        for (uint32_t z = 0; z < Q.samples; ++z) cnt += atomicAdd(&ctr->batch_full, 0u) & 1u;
-#endif
                     bt = atomicAdd(counter, cnt);
                 }
             }
@@ -2425,9 +2256,6 @@ RT_DEV bool finish_segment(const DevScene& S, const DevParams& P, const ChunkPar
         PROF_T0(pm);
         V em = m.kind == rtdev::kMatLight ? tex_value(S, m.tex, rec.u, rec.v, rec.p) : mk(0.0f, 0.0f, 0.0f);
         L = L + T * em;
-#if defined(RT_EXP_PERTURB) && RT_EXP_PERTURB == 5
-        if (P.tune & (1u << 30)) L = L + T * tex_value(S, m.tex, rec.u, rec.v, rec.p);  // never
-#endif
         PROF_ADD(kPrEmit, pm);
         V att;
         Ray sc;
@@ -2715,15 +2543,6 @@ __global__ __launch_bounds__(64, kWaves) void trace_samples(DevScene Sg, DevCame
             bool replay = false;
             PROF_T0(pw);
             bool any = world_hit<kKind, kF>(S, P.prune_delta, ray, g, k, t, he, hc, stk, mode, replay);
-#if defined(RT_EXP_PERTURB) && RT_EXP_PERTURB == 10
-            if ((mode & (1u << 30)) && any) {  // never: the walk again from the hit, as a shadow test
-                Ray r2 = ray;
-                r2.o = at(ray, t);
-                float t2;
-                uint32_t he2 = 0, hc2 = 0;
-                if (world_hit<kKind, kF>(S, P.prune_delta, r2, g, k, t2, he2, hc2, stk, mode, replay)) L = L + mk(t2, t2, t2);
-            }
-#endif
             PROF_ADD(kPrWorld, pw);
             if (kKind == 0 && replay) {  // hand the sample to the reference kernel
                 unsigned idx = atomicAdd(&ctr->replay_count, 1u);
