@@ -281,31 +281,34 @@ struct Key {
     uint32_t k0, k1;
 };
 
-#ifdef RT_PHILOX_INLINE
-__device__ __forceinline__
-#else
+// Inlined in every product unit (round 4, with the SLP vectorizer off: C1 +3%, C4 +4.6% over the
+// out-of-line call the main unit used to make; profiles/r04/experiments/philox_inline_ab_*.log).
+// RT_PHILOX_CALL builds the out-of-line form (the EXEC-join fixture, below).
+#ifdef RT_PHILOX_CALL
 __device__ __noinline__
+#else
+__device__ __forceinline__
 #endif
 uint4 philox_block(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t k0, uint32_t k1) {
     uint32_t c3 = 0u;
     philox(c0, c1, c2, c3, k0, k1);
     return make_uint4(c0, c1, c2, c3);
 }
-// RT_RNG_UNIFORM (the main translation unit, where philox_block is an out-of-line call): the
+// RT_RNG_UNIFORM (the default when philox_block is an out-of-line call, RT_PHILOX_CALL): the
 // block is computed under a wave-uniform branch (any active lane needs one) and taken per
 // lane by select, so no divergent join carries the buffer. With the per-lane branch around
 // the call, ROCm 7.2's VGPR allocator split the buffer's live ranges at the top of the join,
 // ahead of its EXEC restore, so the copies moved r0 / r2 for the calling lanes only and the
-// others' next draw was wrong (the C1 / C4 builds that left the oracle's bits; DESIGN.md §5,
-// tools/exec_join_check.py, which tests/test_exec_join.py runs on every product build). The
-// wave runs the call whenever any lane needs it in either form; the selects cost C4 nothing
-// measurable. The inlined-Philox units keep the per-lane branch (no call, no such split
-// there; the uniform form measured C3 -1.8%, C5 -1.2%) and are covered by the same check.
+// others' next draw was wrong (the C1 / C4 builds that left the oracle's bits).
+// librtamd_rngdiv.so is that build, kept as the regression fixture of tools/exec_join_check.py,
+// which tests/test_exec_join.py runs on every product build. The product inlines Philox (no
+// call at the join) and keeps the per-lane branch, which measured 1-2% faster than the uniform
+// form in the inlined units (C3, C5; rng_uniform_fix_ab_*.log).
 #ifndef RT_RNG_UNIFORM
-#ifdef RT_PHILOX_INLINE
-#define RT_RNG_UNIFORM 0
-#else
+#ifdef RT_PHILOX_CALL
 #define RT_RNG_UNIFORM 1
+#else
+#define RT_RNG_UNIFORM 0
 #endif
 #endif
 RT_DEV uint32_t next_u32(Rng& g, const Key& k) {
@@ -2685,8 +2688,7 @@ void* rt_mc_trace_instance(uint32_t preset) {
     return nullptr;
 }
 #elif defined(RT_INSTANCES_TU) && RT_INSTANCES_TU == 2
-// kernel_flat.hip: the flat-list preset (no BVH, no long sphere runs: C5) with
-// philox_block inlined (RT_PHILOX_INLINE).
+// kernel_flat.hip: the flat-list preset (no BVH, no long sphere runs: C5), camera read from memory.
 void* rt_flat_trace_instance(int waves) {
     return waves == 4 ? reinterpret_cast<void*>(trace_samples<0, 4, 0u>) : reinterpret_cast<void*>(trace_samples<0, 3, 0u>);
 }
@@ -2788,9 +2790,8 @@ using TraceKernel = void (*)(DevScene, DevCamera, DevParams, ChunkParams, float*
 // come from kernel_mc.hip, compiled with the memory-clause scheduling strategy:
 // measured on the same box it is 1.3% faster on C3 and 1.2% on C2 but 1-2% slower
 // on the other presets (C4, C5), and a scheduling strategy is a per-file flag.
-// The flat-list instances come from kernel_flat.hip, where philox_block is inlined: the
-// call's register saves cost that preset 8% (C5 151 -> 140 ms per 200-spp frame, same box),
-// while the BVH presets are 1-2% slower with it inlined (C3, C4) and C2 is unchanged.
+// The flat-list instances come from kernel_flat.hip, which reads the camera from its device
+// copy (RT_CAMMEM).
 template <int kWaves, uint32_t kF>
 TraceKernel preset_instance() {
 #ifdef RT_SPLIT_MC
