@@ -1003,7 +1003,9 @@ struct Trav {
     uint32_t cur, sp, best_rank;
     float tmax_entry;
     bool any;
+    uint32_t pend;  // a leaf node reached and not yet tested (kNoNode: none; bvh_run)
 };
+constexpr uint32_t kNoNode = 0xffffffffu;
 // Audit build: every completed fast traversal is replayed with the reference recursion
 // (bvh_hit_reference, on the lane's now free LDS stack); disagreements are recorded.
 RT_DEV void trav_audit(const DevScene& S, const f4* wrapper, uint32_t root, const Ray& r, V inv, float tmin,
@@ -1033,6 +1035,9 @@ RT_DEV void trav_audit(const DevScene& S, const f4* wrapper, uint32_t root, cons
 #define RT_SUSP_MIN_TRIPS 2
 #endif
 constexpr uint32_t kSuspMinTrips = RT_SUSP_MIN_TRIPS;
+#ifndef RT_LEAF_Q
+#define RT_LEAF_Q 8
+#endif
 template <int kKind, uint32_t kF, bool kSusp>
 RT_DEV bool bvh_run(const DevScene& S, float delta, const f4* wrapper, const Ray& r, V inv, float tmin, float& closest,
                     uint32_t& hit_code, uint32_t* stk, uint32_t mode, Trav& tv, uint32_t susp);
@@ -1076,7 +1081,7 @@ RT_DEV bool bvh_hit(const DevScene& S, float delta, uint32_t root, const Ray& r,
         }
     }
     PROF_ADD(kPrBvhSetup, psetup);
-    Trav tv{root, 0u, 0u, closest, false};
+    Trav tv{root, 0u, 0u, closest, false, kNoNode};
     bvh_run<kKind, kF, false>(S, delta, wrapper, r, inv, tmin, closest, hit_code, stk, mode, tv, 0u);
     const bool any = tv.any;
     PROF_ADD(kPrBvhCall, pcall);
@@ -1106,7 +1111,22 @@ RT_DEV bool bvh_run(const DevScene& S, float delta, const f4* wrapper, const Ray
     [[maybe_unused]] const uint32_t hnx = inv.x < 0.0f ? 48u : 0u, hny = inv.y < 0.0f ? 64u : 16u,
                                     hnz = inv.z < 0.0f ? 80u : 32u;
     bool any = tv.any;
-    uint32_t best_rank = tv.best_rank, sp = tv.sp, cur = tv.cur;
+    uint32_t best_rank = tv.best_rank, sp = tv.sp, cur = tv.cur, pend = tv.pend;
+    // Leaf postponement (the triangle preset; q = RT_LEAF_Q sixteenths, RT_OPT_TUNE bits 24-27
+    // override it for A/B, 15 = off): a lane that reaches a leaf node parks it in `pend` and goes
+    // on with the next node of its stack; the wave tests the parked leaves together once at least
+    // q/16 of its traversing lanes hold one, or when no lane can advance otherwise. The leaf test
+    // ran at a few lanes per execution when every lane tested its leaf at once. Every candidate
+    // still meets the same tests and merges into (closest, DFS rank) by the same order-independent
+    // rule, and pruning stays conservative with a later `closest`, so the result is the same bits;
+    // only the visit order changes. Measured (same box, bit-identical, 50-spp C4 frames): 1061 ->
+    // 1094 Msamples/s at q = 8 (q = 4: 1093, 6: 1097, 10: 1080); on the sphere presets, where a
+    // leaf hit prunes the rest of the stack, no q beat testing at once (runtime-q build: C3 q = 8
+    // -1.4%, C1 -3%), so they compile the immediate loop, instruction for instruction the old one
+    // (profiles/r04/experiments/leaf_postpone_*.log).
+    constexpr bool kPostpone = (kF & kFTri) != 0u && kKind == 0;
+    const uint32_t tq = (mode >> 24) & 15u;
+    const uint32_t lq = !kPostpone ? 0u : (tq == 15u ? 0u : (tq ? tq : (uint32_t)RT_LEAF_Q));
     bool finished = true;
     [[maybe_unused]] uint32_t trips = 0;
 #ifdef RT_PROFILE_REGIONS
@@ -1120,10 +1140,37 @@ RT_DEV bool bvh_run(const DevScene& S, float delta, const f4* wrapper, const Ray
             }
             ++trips;
         }
-        // One batch of loads per step: a leaf node needs the .xy halves of its
-        // rows, an interior node its six box rows and child codes.
-        const bool leaf_node = (cur & rtdev::kLeafNodeFlag) != 0u;
-        const uint32_t nbo = (cur & ~rtdev::kLeafNodeFlag) * (rtdev::kBvhNodeF4 * 16u);  // node byte offset
+        // this trip: test one leaf node (the parked one first), or park the current leaf, or
+        // visit the current interior node. Without postponement `cur` is always a node here.
+        uint32_t lnode = kNoNode;
+        bool popnext = false, do_int;
+        if constexpr (kPostpone) {
+            const bool cur_leaf = cur != kNoNode && (cur & rtdev::kLeafNodeFlag) != 0u;
+            const bool has_pend = pend != kNoNode;
+            bool leafphase = true;
+            if (lq) {
+                const bool can_adv = cur != kNoNode && (!cur_leaf || !has_pend);
+                const uint32_t n_act = (uint32_t)__popcll(__ballot(1)), n_pend = (uint32_t)__popcll(__ballot(has_pend));
+                leafphase = __ballot(can_adv) == 0ull || n_pend * 16u >= lq * n_act;
+            }
+            if (leafphase) {
+                if (has_pend) {
+                    lnode = pend;
+                    pend = kNoNode;
+                } else if (cur_leaf) {
+                    lnode = cur;
+                    popnext = true;
+                }
+            } else if (cur_leaf && !has_pend) {
+                pend = cur;
+                popnext = true;
+            }
+            do_int = lnode == kNoNode && !popnext && cur != kNoNode && !cur_leaf;
+        } else {
+            const bool cur_leaf = (cur & rtdev::kLeafNodeFlag) != 0u;
+            lnode = cur_leaf ? cur : kNoNode;
+            do_int = !cur_leaf;
+        }
         // The near-plane row offsets. The sphere-BVH presets rederive them each trip from the
         // direction's sign bits (volatile asm is not hoisted: three loop-invariant offsets live
         // across the loop, where registers are scarcest, pushed C3's sample-loop state into
@@ -1143,16 +1190,19 @@ RT_DEV bool bvh_run(const DevScene& S, float delta, const f4* wrapper, const Ray
             onz = (msz & 48u) + 32u;
         }
 #ifdef RT_LEAF_AUDIT
-        if ((cur & ~rtdev::kLeafNodeFlag) >= S.num_nodes || sp > S.stack_depth + S.spill_depth) {
-            atomicAdd(&g_bounds_audit_count, 1u);
-            break;
+        {
+            const uint32_t vis = lnode != kNoNode ? lnode : cur;
+            if ((vis != kNoNode && (vis & ~rtdev::kLeafNodeFlag) >= S.num_nodes) || sp > S.stack_depth + S.spill_depth) {
+                atomicAdd(&g_bounds_audit_count, 1u);
+                break;
+            }
         }
 #endif
 #ifdef RT_PROFILE_REGIONS
         ++visits;
 #endif
         PROF_T0(pt);
-        if (leaf_node) {
+        if (lnode != kNoNode) {
             // The 1-2 leaf children of ONE reference BVH2 node, left then right,
             // and that node's result formed exactly like bvh.rs:377-414: the left
             // leaf is tested with the BVH's entry t_max, the right one with the
@@ -1162,6 +1212,7 @@ RT_DEV bool bvh_run(const DevScene& S, float delta, const f4* wrapper, const Ray
             // rounded t equals another candidate's passes or fails depending on
             // which t_max it saw. The node result then joins (closest, DFS rank)
             // like the tree-min does.
+            const uint32_t nbo = (lnode & ~rtdev::kLeafNodeFlag) * (rtdev::kBvhNodeF4 * 16u);  // node byte offset
             const f4* nd = S.nodes;
             const float2 nx2 = ld2_at(nd, nbo + onx), ny2 = ld2_at(nd, nbo + ony), nz2 = ld2_at(nd, nbo + onz),
                          fx2 = ld2_at(nd, nbo + (onx ^ 48u)), fy2 = ld2_at(nd, nbo + (ony ^ 80u)),
@@ -1222,8 +1273,9 @@ RT_DEV bool bvh_run(const DevScene& S, float delta, const f4* wrapper, const Ray
         }
         float t0 = kInf, t1 = kInf, t2 = kInf, t3 = kInf;
         uint32_t c0 = rtdev::kChildEmpty, c1 = rtdev::kChildEmpty, c2 = rtdev::kChildEmpty, c3 = rtdev::kChildEmpty;
-        if (!leaf_node) {
+        if (do_int) {
             // interior slots: reference box test, prune bound, nearest first
+            const uint32_t nbo = cur * (rtdev::kBvhNodeF4 * 16u);  // node byte offset
             const f4* nd = S.nodes;
             const f4 nx = ld4_at(nd, nbo + onx), ny = ld4_at(nd, nbo + ony), nz = ld4_at(nd, nbo + onz),
                      fx = ld4_at(nd, nbo + (onx ^ 48u)), fy = ld4_at(nd, nbo + (ony ^ 80u)),
@@ -1272,40 +1324,56 @@ RT_DEV bool bvh_run(const DevScene& S, float delta, const f4* wrapper, const Ray
         sort2(t0, c0, t2, c2);
         sort2(t1, c1, t3, c3);
         sort2(t1, c1, t2, c2);
-        if (t0 != kInf) {  // visit the nearest now, push the others far to near
+        if (t0 != kInf) {  // visit the nearest next, push the others far to near
             if (t3 != kInf) push(c3, t3);
             if (t2 != kInf) push(c2, t2);
             if (t1 != kInf) push(c1, t1);
             cur = c0;
-            PROF_ADD(kPrBvhPush, pp);
-            continue;
+            if constexpr (!kPostpone) {
+                PROF_ADD(kPrBvhPush, pp);
+                continue;
+            }
+        } else if (!kPostpone || do_int) {
+            popnext = true;
         }
         PROF_ADD(kPrBvhPush, pp);
         PROF_T0(ppop);
-        bool found = false;
-        while (sp > 0u) {
-            sp -= 1u;
-            uint32_t cand;
-            float tenter;
-            if (!(kF & kFDeep) || sp < S.stack_depth) {
-                cand = stk[sp * 128u];
-                tenter = __uint_as_float(stk[sp * 128u + 64u]);
-            } else {
-                const uint32_t* g = S.stack_spill +
-                                    (((size_t)blockIdx.x * S.spill_depth + (sp - S.stack_depth)) * 64u + threadIdx.x) * 2u;
-                cand = g[0];
-                tenter = __uint_as_float(g[1]);
+        if (popnext) {
+            bool found = false;
+            while (sp > 0u) {
+                sp -= 1u;
+                uint32_t cand;
+                float tenter;
+                if (!(kF & kFDeep) || sp < S.stack_depth) {
+                    cand = stk[sp * 128u];
+                    tenter = __uint_as_float(stk[sp * 128u + 64u]);
+                } else {
+                    const uint32_t* g = S.stack_spill +
+                                        (((size_t)blockIdx.x * S.spill_depth + (sp - S.stack_depth)) * 64u + threadIdx.x) * 2u;
+                    cand = g[0];
+                    tenter = __uint_as_float(g[1]);
+                }
+                if (!prune || !(tenter > prune_bound(closest))) {
+                    cur = cand;
+                    found = true;
+                    break;
+                }
             }
-            if (!prune || !(tenter > prune_bound(closest))) {
-                cur = cand;
-                found = true;
-                break;
+            if (!found) {
+                if constexpr (!kPostpone) {
+                    PROF_ADD(kPrBvhPop, ppop);
+                    break;
+                } else {
+                    cur = kNoNode;
+                }
             }
         }
         PROF_ADD(kPrBvhPop, ppop);
-        if (!found) break;
+        if constexpr (kPostpone) {
+            if (cur == kNoNode && pend == kNoNode) break;
+        }
     }
-    tv = Trav{cur, sp, best_rank, tmax_entry, any};
+    tv = Trav{cur, sp, best_rank, tmax_entry, any, pend};
 #ifdef RT_PROFILE_REGIONS
     {
         const uint32_t b = trips_bin(visits);
@@ -2003,7 +2071,7 @@ RT_DEV void world_walk(const DevScene& S, float delta, const Ray& ray, Rng& g, c
                     w.pos = S.num_top + 1u;  // abandoned: the sample is re-traced by the reference kernel
                     continue;
                 }
-                w.tv = Trav{root, 0u, 0u, w.closest, false};
+                w.tv = Trav{root, 0u, 0u, w.closest, false, kNoNode};
             }
             if (bvh_run<0, kF, true>(S, delta, wrapper, r, inv, 0.001f, w.closest, w.hit_code, stk, mode, w.tv, susp)) {
                 trav_audit(S, wrapper, root, r, inv, 0.001f, w.tv, w.closest, w.hit_code, stk);
