@@ -45,27 +45,11 @@ def test_checker_finds_the_rng_buffer_copies_in_the_fixture():
     per = {}
     for fn, join, what in found:
         per.setdefault(kr.readable(fn), []).append(what.split(": ", 1)[1])
-    # the BVH-only (C1) and triangle (C4) instances of kernel.hip, where philox_block is a call:
-    # two v_mov copies each, r0 and r2 of the buffer, at the join of the time draw's block fetch
-    assert set(per) == {"trace_samples<0, 3, 1>", "trace_samples<0, 3, 75>"}, per
+    # kernel.hip's instances that the fixture's allocator split that way: the C1 instance (which
+    # tests/test_gpu_exec_join.py renders) among them, two v_mov copies (r0, r2 of the buffer)
+    # at the join of the time draw's block fetch in each; which other instances show it moves
+    # with unrelated code (round 4: the triangle preset's, later the all-feature ones)
+    assert "trace_samples<0, 3, 1>" in per, per
     for inst, ops in per.items():
+        assert inst.startswith("trace_samples<0,"), (inst, ops)
         assert len(ops) == 2 and all(o.startswith("v_mov_b32") for o in ops), (inst, ops)
-
-
-def test_classifier_on_synthetic_lines():
-    ins = ejc.parse("\n".join([
-        "0000000000000000 <k>:",
-        "\ts_and_saveexec_b64 s[14:15], vcc                          // 000000000000: BE8E206A",
-        "\ts_cbranch_execz 2                                           // 000000000004: BF880002",
-        "\tv_mov_b32_e32 v1, v2                                        // 000000000008: 7E020302",
-        "\tv_add_u32_e32 v3, 1, v3                                     // 00000000000C: 68060681",
-        "\tv_mov_b32_e32 v4, v2                                        // 000000000010: 7E080302",
-        "\ts_or_b64 exec, exec, s[14:15]                               // 000000000014: 87FE0E7E",
-    ]))
-    assert [m for _, _, m, _ in ins] == ["s_and_saveexec_b64", "s_cbranch_execz", "v_mov_b32_e32", "v_add_u32_e32",
-                                         "v_mov_b32_e32", "s_or_b64"]
-    assert ejc.narrows_exec("s_and_saveexec_b64", "s[14:15], vcc")
-    assert not ejc.narrows_exec("s_or_b64", "exec, exec, s[14:15]")
-    assert ejc.writes_exec("s_or_b64", "exec, exec, s[14:15]")
-    assert ejc.writes_vgpr("v_mov_b32_e32", "v4, v2") and not ejc.writes_vgpr("v_readlane_b32", "s0, v142, 3")
-    assert not ejc.writes_vgpr("v_cmp_eq_u32_e32", "vcc, 0, v1")
