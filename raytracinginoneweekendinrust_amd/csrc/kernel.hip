@@ -80,6 +80,8 @@ constexpr uint32_t kModePruneAllExp = 1u << 20;
 // 8: C3 69.7 -> 68.0 ms, C1 -3%). BlocksForward (RT_OPT_TUNE, A/B only) restores
 // the top-first order. Either order gives the same bits (samples are keyed by pixel and index).
 constexpr uint32_t kModeBlocksForward = 1u << 21;
+// W4 (RT_OPT_TUNE, A/B only): the 4-wave instance also for the presets that prefer 3 (below).
+constexpr uint32_t kModeW4 = 1u << 22;
 #ifdef RT_ABLATE
 // Ablation build (librtamd_ablate.so, diagnostics only): RT_OPT_TUNE bits that run a
 // piece of work twice (results of the copy discarded through an opaque test),
@@ -3361,7 +3363,7 @@ int rt_render_launch_camera(rt_scene_handle s, const rt_camera* camera, const rt
         const TraceKernel k3 = fast_instance(3, s->features), k4 = fast_instance(4, s->features);
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per3, k3, 64, stack_lds + perm3) != hipSuccess) per3 = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per4, k4, 64, stack_lds) != hipSuccess) per4 = 0;
-        s->fast_waves = per4 > per3 && !(dp.tune & kModeW3) && !prefer3 ? 4 : 3;
+        s->fast_waves = per4 > per3 && !(dp.tune & kModeW3) && (!prefer3 || (dp.tune & kModeW4)) ? 4 : 3;
     }
     if (s->fast_waves == 4) dp.tune |= kModeNoPermLds;
     // LDS per wave: the kernel's traversal stack, then the Perlin tables
