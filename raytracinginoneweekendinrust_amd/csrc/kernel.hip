@@ -343,6 +343,14 @@ RT_DEV float std01(Rng& g, const Key& k) {  // rand 0.8.5 Standard f32
     return (1.0f / 16777216.0f) * (float)(next_u32(g, k) >> 8);
 }
 RT_DEV float from_1_2(uint32_t u) { return __uint_as_float((u >> 9) | 0x3f800000u); }
+// UniformFloat::sample_single for gen_range(-1.0..1.0) (utils.rs's only ranges on the path):
+// v01 * scale + low with scale = 2, low = -1. Its retry (res >= high) never fires for this
+// range: from_1_2(u) - 1 lies in [0, 1 - 2^-23], times 2 is exact, minus 1 gives
+// [-1, 1 - 2^-22] exactly, always < 1; so one word is one value.
+[[maybe_unused]] RT_DEV float range_pm1(uint32_t u) { return (from_1_2(u) - 1.0f) * 2.0f + -1.0f; }
+#ifdef RT_SEQ_DRAWS
+// Sequential draws (the EXEC-join regression fixture, librtamd_rngdiv.so, is built this way: the
+// form of round 3 and early round 4, one next_u32 per coordinate with rand's retry loop).
 RT_DEV float range_f(Rng& g, const Key& k, float low, float high) {  // UniformFloat::sample_single
     float scale = high - low;
     for (;;) {
@@ -369,6 +377,56 @@ RT_DEV V in_unit_disk(Rng& g, const Key& k) {  // utils.rs:9-17
         if (dot(p, p) < 1.0f) return p;
     }
 }
+#else
+// gen_range(-1.0..1.0) never retries (range_pm1), so every attempt of in_unit_sphere takes
+// exactly the words d, d+1, d+2 of the stream, at most one Philox block beyond the buffer:
+// j = d % 4 = 0 -> block d/4 words 0-2; 1 -> the buffered words 1-3; 2 -> buffered 2, 3 and word 0
+// of block d/4 + 1; 3 -> buffered 3 and words 0, 1 of the next block. The attempt computes that
+// block once, under a wave-uniform branch, where three sequential draws ran Philox whenever any
+// lane crossed a block boundary, i.e. up to three times per attempt for a wave whose lanes are
+// out of phase. The words and the buffer it leaves are those of the sequential draws.
+RT_DEV V in_unit_sphere(Rng& g, const Key& k) {  // materials/utils.rs:6-19
+    for (;;) {
+        const uint32_t j = g.d & 3u;
+        uint4 b = make_uint4(g.r0, g.r1, g.r2, g.r2);
+        if (__ballot(j != 1u) != 0ull) b = philox_block((g.d + 2u) >> 2, g.sample, g.pixel, k.k0, k.k1);
+        const bool j0 = j == 0u, j1 = j == 1u, j2 = j == 2u;
+        const uint32_t u0 = j0 ? b.x : g.r0;
+        const uint32_t u1 = j0 ? b.y : (j1 || j2 ? g.r1 : b.x);
+        const uint32_t u2 = j0 ? b.z : (j1 ? g.r2 : (j2 ? b.x : b.y));
+        const uint32_t n0 = j0 ? b.w : (j1 ? g.r2 : (j2 ? b.y : b.z));
+        const uint32_t n1 = j0 ? b.w : (j1 ? g.r2 : (j2 ? b.z : b.w));
+        const uint32_t n2 = j1 ? g.r2 : b.w;
+        g.r0 = n0;
+        g.r1 = n1;
+        g.r2 = n2;
+        g.d += 3u;
+        V v = mk(range_pm1(u0), range_pm1(u1), range_pm1(u2));
+        if (dot(v, v) < 1.0f) return v;
+    }
+}
+// The same for the lens disk's two words per attempt: j = 0 -> block d/4 words 0, 1; 1, 2 ->
+// the buffered words; 3 -> buffered word 3 and word 0 of the next block.
+RT_DEV V in_unit_disk(Rng& g, const Key& k) {  // utils.rs:9-17
+    for (;;) {
+        const uint32_t j = g.d & 3u;
+        uint4 b = make_uint4(g.r0, g.r1, g.r2, g.r2);
+        if (__ballot(j == 0u || j == 3u) != 0ull) b = philox_block((g.d + 1u) >> 2, g.sample, g.pixel, k.k0, k.k1);
+        const bool j0 = j == 0u, j3 = j == 3u;
+        const uint32_t u0 = j0 ? b.x : g.r0;
+        const uint32_t u1 = j0 ? b.y : (j3 ? b.x : g.r1);
+        const uint32_t n0 = j0 ? b.z : (j3 ? b.y : g.r2);
+        const uint32_t n1 = j0 ? b.w : (j3 ? b.z : g.r2);
+        const uint32_t n2 = j0 || j3 ? b.w : g.r2;
+        g.r0 = n0;
+        g.r1 = n1;
+        g.r2 = n2;
+        g.d += 2u;
+        V p = mk(range_pm1(u0), range_pm1(u1), 0.0f);
+        if (dot(p, p) < 1.0f) return p;
+    }
+}
+#endif
 
 // ---------------------------------------------------------------------------
 // primitive tests: return the parameter t of the first valid root only
@@ -554,6 +612,7 @@ constexpr uint32_t kFBvh = 1u, kFTri = 2u, kFRuns = 4u, kFDeep = 8u, kFLeafRM = 
 // Measured on the same box (50-spp frames): C4 197 -> 128 ms; the flat / sphere-BVH presets
 // are 5-8% slower with it (C3 124 -> 133 ms, C5 152 -> 160 ms), so only that preset uses it.
 constexpr uint32_t kFSusp = 64u;
+
 [[maybe_unused]] constexpr uint32_t kStackLdsMax = 19u;  // LDS stack entries per lane at most (9.5 KB per wave: 16 waves/CU)
 // One leaf (primitive or cube). tmax = closest so far; a hit with t == closest is
 // accepted, so later candidates win ties exactly like hittable.rs:110-116.
@@ -3465,8 +3524,12 @@ int rt_render_launch_camera(rt_scene_handle s, const rt_camera* camera, const rt
                                s->sbuf, s->counter, s->replay, 0u, d_segments);
         } else {  // fast kernel, then the reference kernel on the samples it handed over
             const TraceKernel kf = fast_instance(s->fast_waves, s->features);
-            const bool kind3 = !(s->features & kFDeep) && !(dp.tune & kModeReplayRef);
-            const bool stream_rp = kind3 && !(dp.tune & kModeNoStream);
+            // A deep-stack scene (C4) replays with trace_samples<3, 3, kFAll>, after the fast kernel:
+            // its BVH4 traversals spill into the fast kernel's HBM slabs, free by then, so the
+            // launch keeps to the fast kernel's grid; the streaming pass would share those slabs.
+            const bool deep = (s->features & kFDeep) != 0u;
+            const bool kind3 = !(dp.tune & kModeReplayRef);
+            const bool stream_rp = kind3 && !deep && !(dp.tune & kModeNoStream);
             if (stream_rp && (e = hipEventRecord(s->fork, st)) != hipSuccess) return hip_fail(e, "replay stream fork");
             hipLaunchKernelGGL(kf, dim3(grid), dim3(64), lds, st, s->dev, cam, dp, q, s->sbuf, s->counter, s->replay,
                                0u, d_segments);
@@ -3487,8 +3550,12 @@ int rt_render_launch_camera(rt_scene_handle s, const rt_camera* camera, const rt
                         return hip_fail(e, "replay stream join");
                 }
                 // serialized: whatever the streaming pass did not take (everything without it)
-                hipLaunchKernelGGL((trace_samples<3, 3, kFAll & ~kFDeep>), dim3(grid_ref), dim3(64), lds_rp, st,
-                                   dev_rp, cam, dp, q, s->sbuf, s->counter, s->replay, 1u, d_segments);
+                if (deep)
+                    hipLaunchKernelGGL((trace_samples<3, 3, kFAll>), dim3(std::min(grid_ref, grid)), dim3(64), lds_rp, st,
+                                       dev_rp, cam, dp, q, s->sbuf, s->counter, s->replay, 1u, d_segments);
+                else
+                    hipLaunchKernelGGL((trace_samples<3, 3, kFAll & ~kFDeep>), dim3(grid_ref), dim3(64), lds_rp, st,
+                                       dev_rp, cam, dp, q, s->sbuf, s->counter, s->replay, 1u, d_segments);
             } else {
                 hipLaunchKernelGGL(trace_samples<1>, dim3(grid_ref), dim3(64), lds_ref, st, dev_ref, cam, dp, q,
                                    s->sbuf, s->counter, s->replay, 1u, d_segments);
