@@ -3471,8 +3471,9 @@ int rt_render_launch_camera(rt_scene_handle s, const rt_camera* camera, const rt
             cus = 256;
         s->grid = per_cu * cus;
         s->grid_ref = per_cu_ref * cus;
-        if (s->features & kFDeep) {  // the deep-stack spill area: one slab per resident wave
-            const size_t bytes = (size_t)s->grid * s->dev.spill_depth * 64u * 2u * sizeof(uint32_t);
+        if (s->features & kFDeep) {  // the deep-stack spill area: one slab per resident wave, then
+            // kStreamWaves slabs for the streaming replay pass, which runs beside the fast kernel
+            const size_t bytes = ((size_t)s->grid + kStreamWaves) * s->dev.spill_depth * 64u * 2u * sizeof(uint32_t);
             if ((e = hipMalloc(&s->stack_spill, bytes)) != hipSuccess) {
                 s->grid = 0;
                 return rthost::set_error(RT_ERR_OOM, std::string("hipMalloc stack spill: ") + hipGetErrorString(e));
@@ -3526,12 +3527,12 @@ int rt_render_launch_camera(rt_scene_handle s, const rt_camera* camera, const rt
                                s->sbuf, s->counter, s->replay, 0u, d_segments);
         } else {  // fast kernel, then the reference kernel on the samples it handed over
             const TraceKernel kf = fast_instance(s->fast_waves, s->features);
-            // A deep-stack scene (C4) replays with trace_samples<3, 3, kFAll>, after the fast kernel:
-            // its BVH4 traversals spill into the fast kernel's HBM slabs, free by then, so the
-            // launch keeps to the fast kernel's grid; the streaming pass would share those slabs.
+            // A deep-stack scene (C4) replays with trace_samples<3, 3, kFAll>: the streaming pass
+            // spills into its own slabs behind the fast kernel's, the serialized remainder into the
+            // fast kernel's, free by then (so that launch keeps to the fast kernel's grid).
             const bool deep = (s->features & kFDeep) != 0u;
             const bool kind3 = !(dp.tune & kModeReplayRef);
-            const bool stream_rp = kind3 && !deep && !(dp.tune & kModeNoStream);
+            const bool stream_rp = kind3 && !(dp.tune & kModeNoStream);
             if (stream_rp && (e = hipEventRecord(s->fork, st)) != hipSuccess) return hip_fail(e, "replay stream fork");
             hipLaunchKernelGGL(kf, dim3(grid), dim3(64), lds, st, s->dev, cam, dp, q, s->sbuf, s->counter, s->replay,
                                0u, d_segments);
@@ -3545,8 +3546,15 @@ int rt_render_launch_camera(rt_scene_handle s, const rt_camera* camera, const rt
                     // drain they overlap by a third)
                     const uint32_t grid_st = std::min(grid_ref, kStreamWaves);
                     if ((e = hipStreamWaitEvent(s->aux, s->fork, 0)) != hipSuccess) return hip_fail(e, "replay stream wait");
-                    hipLaunchKernelGGL((trace_samples<3, 3, kFAll & ~kFDeep>), dim3(grid_st), dim3(64), lds_rp, s->aux,
-                                       dev_rp, cam, dp, q, s->sbuf, s->counter, s->replay, 2u, d_segments);
+                    if (deep) {
+                        DevScene dev_st = dev_rp;
+                        dev_st.stack_spill = s->stack_spill + (size_t)s->grid * s->dev.spill_depth * 64u * 2u;
+                        hipLaunchKernelGGL((trace_samples<3, 3, kFAll>), dim3(grid_st), dim3(64), lds_rp, s->aux, dev_st,
+                                           cam, dp, q, s->sbuf, s->counter, s->replay, 2u, d_segments);
+                    } else {
+                        hipLaunchKernelGGL((trace_samples<3, 3, kFAll & ~kFDeep>), dim3(grid_st), dim3(64), lds_rp,
+                                           s->aux, dev_rp, cam, dp, q, s->sbuf, s->counter, s->replay, 2u, d_segments);
+                    }
                     if ((e = hipEventRecord(s->join, s->aux)) != hipSuccess ||
                         (e = hipStreamWaitEvent(st, s->join, 0)) != hipSuccess)
                         return hip_fail(e, "replay stream join");
