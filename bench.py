@@ -33,6 +33,9 @@ for _p in (ROOT, os.path.join(ROOT, "oracle")):
 
 METRIC = "Msamples/s (rays traced/s) + HBM GB/s vs roofline, showcase@1200x800x500spp"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md "Chip-level parameters"
+# rows shared by every workgroup, served by each XCD's L2: 16.8-18.8 TB/s chip-wide (the top of the range),
+# MI355X_MICROARCH.md "Indexed rows: gather into LDS"
+L2_PEAK_GBS = 18800.0
 
 # Algorithmic bytes per unit: 32 B per BVH node visit, per-primitive
 # record sizes, 32 B material record per hit, 3 B per image texel, 12 B framebuffer per pixel.
@@ -56,6 +59,34 @@ def host_nproc() -> int:
     """The CPUs this process may run on (its affinity mask: what `nproc` prints, without
     starting a program from a GPU-initialised process)."""
     return len(os.sched_getaffinity(0))
+
+
+def cpu_share():
+    """The CPU time this process's cgroup may use, in CPUs (cgroup v2 cpu.max or v1
+    cfs_quota/cfs_period), and where it was read; (None, reason) without a quota."""
+    paths = ["/sys/fs/cgroup/cpu.max"]
+    try:  # cgroup v2: this process's own group first ("0::/path" in /proc/self/cgroup)
+        for line in open("/proc/self/cgroup"):
+            if line.startswith("0::"):
+                paths.insert(0, "/sys/fs/cgroup" + line.strip()[3:].rstrip("/") + "/cpu.max")
+    except Exception:
+        pass
+    for path in paths:
+        try:
+            quota, period = open(path).read().split()[:2]
+            if quota == "max":
+                return None, f"{path}: max (no quota)"
+            return int(quota) / int(period), f"{path}: {quota} {period}"
+        except Exception:
+            pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        if q > 0:
+            return q / per, f"cpu.cfs_quota_us {q} / cpu.cfs_period_us {per}"
+        return None, "cpu.cfs_quota_us -1 (no quota)"
+    except Exception:
+        return None, "no cgroup cpu quota readable"
 
 
 def cpu_threads() -> int:
@@ -240,11 +271,22 @@ def main() -> int:
         try:
             cnt = oracle_measure(cfg, scene, threads, full=c1)
             if world == 1 and not args.no_cpu_baseline:
-                cpu = {"value": cnt["samples"] / cnt["seconds"] / 1e6, "unit": "Msamples/s", "cores": cnt["threads"],
-                       "kind": "port", "label": "oracle restatement (C, pthreads)", "host_nproc": host_nproc(),
+                v = cnt["samples"] / cnt["seconds"] / 1e6
+                share, share_src = cpu_share()
+                nproc = host_nproc()
+                cpu = {"value": v, "unit": "Msamples/s", "cores": cnt["threads"],
+                       "kind": "port", "label": "oracle restatement (C, pthreads)", "host_nproc": nproc,
+                       "cpu_quota_cpus": share, "cpu_quota_source": share_src,
+                       "per_core": v / cnt["threads"],
+                       # rayon's par_iter over every logical CPU (src/renderer.rs:63-85) on the whole host:
+                       # NOT measured (the box grants this process `cpu_quota_cpus` CPUs of CPU time, and
+                       # the pool asks for worker pools sized to that share); the per-thread rate times
+                       # host_nproc, i.e. perfect linear scaling, an upper bound for the reference's CPU path
+                       "host_nproc_linear_extrapolation": v / cnt["threads"] * nproc,
                        "note": "the C oracle restatement of the reference (oracle/oracle.c), the Rust reference "
                                "cannot be built here; threads = the affinity mask capped by OMP_NUM_THREADS "
-                               "(the box's CPU share)",
+                               "(the box's CPU share, see cpu_quota_cpus); host_nproc_linear_extrapolation is "
+                               "per_core x host_nproc, not a measurement",
                        "sample": (f"{cfg.name} whole frame ({cnt['samples'] // spp} px)" if c1 else
                                   f"{cfg.name} 8x8 blocks b % {SUBSAMPLE} == 21 ({cnt['samples'] // spp} px, 1/64 of "
                                   f"the frame)") + f" at {spp} spp depth {cfg.depth}: {cnt['samples']} samples in "
@@ -262,6 +304,9 @@ def main() -> int:
         if valu:
             valu = {k: v for k, v in valu.items() if k != "counters"}
         value = total_samples / wall_max / 1e6
+        if cpu:
+            cpu["gpu_over_cpu"] = value / cpu["value"]
+            cpu["gpu_over_host_nproc_extrapolation"] = value / cpu["host_nproc_linear_extrapolation"]
         line = {
             # BASELINE.json's metric is quoted on C3; the other configs name their own workload
             "metric": METRIC if cfg.name == "C3" else
@@ -295,6 +340,8 @@ def main() -> int:
             "frame_md5": frame_md5,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
+                         # the same rate against the XCD L2's measured shared-row rate (the scene's home)
+                         "l2_peak": L2_PEAK_GBS, "l2_frac": (achieved / L2_PEAK_GBS) if achieved else None,
                          "achieved_is": "SURVEY.md §8(d) algorithmic bytes per sample (the reference algorithm's "
                                         "scene reads, counted by the oracle) x samples / trace-kernel time: an "
                                         "L2 scene-read rate (the scene is L2-resident), priced against HBM peak "

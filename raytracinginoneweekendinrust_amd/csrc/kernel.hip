@@ -2855,6 +2855,20 @@ __global__ __launch_bounds__(256) void hrpp_count(const rtdev::HrppSlot* __restr
         }
     }
 }
+// The launch's camera into device memory (RT_CAMMEM instances read it there). The value travels
+// as a kernel argument, captured when the launch is enqueued, so no host buffer has to outlive
+// the call (a hipMemcpyAsync from the caller's stack would rely on the runtime staging pageable
+// copies before it returns).
+__global__ void store_camera(DevCamera c, DevCamera* __restrict__ dst) {
+    constexpr uint32_t kWords = sizeof(DevCamera) / sizeof(uint32_t);
+    static_assert(sizeof(DevCamera) % sizeof(uint32_t) == 0, "DevCamera is whole words");
+    const uint32_t i = threadIdx.x;
+    if (i < kWords) {
+        uint32_t w;
+        __builtin_memcpy(&w, reinterpret_cast<const char*>(&c) + 4u * i, 4u);
+        reinterpret_cast<uint32_t*>(dst)[i] = w;
+    }
+}
 }  // namespace
 
 struct rt_scene {
@@ -3502,9 +3516,12 @@ int rt_render_launch_camera(rt_scene_handle s, const rt_camera* camera, const rt
             return hip_fail(e, "memset counters");
         // the launch's camera behind the counters: the flat-list instances (kernel_flat.hip, RT_CAMMEM)
         // read it from there at each new sample instead of keeping 21 camera words in SGPRs
-        if (c == 0 && (e = hipMemcpyAsync(reinterpret_cast<char*>(s->counter) + kCamOffset, &cam, sizeof cam,
-                                          hipMemcpyHostToDevice, st)) != hipSuccess)
-            return hip_fail(e, "camera copy");
+        if (c == 0) {
+            (void)hipGetLastError();  // sticky: drop an unrelated earlier error
+            hipLaunchKernelGGL(store_camera, dim3(1), dim3(64), 0, st, cam,
+                               reinterpret_cast<DevCamera*>(reinterpret_cast<char*>(s->counter) + kCamOffset));
+            if ((e = hipGetLastError()) != hipSuccess) return hip_fail(e, "camera store");
+        }
         uint32_t grid = (uint32_t)s->grid, grid_ref = (uint32_t)s->grid_ref;
         if (grid > q.units) grid = q.units;
         if (grid_ref > q.units) grid_ref = q.units;

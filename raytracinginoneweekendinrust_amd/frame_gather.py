@@ -43,6 +43,14 @@ import numpy as np
 from . import shard_floats, shard_offset, shard_pack, shard_unpack
 
 SLOTS = 2  # gather-buffer slots, used in alternate steps
+MAX_PULL_RANKS = 64  # rt_shard_pull_unpack's peer table (gather.hip kMaxPullRanks)
+
+
+def block_ranks(width: int, height: int, world: int) -> np.ndarray:
+    """The rank that renders each pixel (row-major H*W): 8x8 block b goes to rank b % world."""
+    bx = (width + 7) // 8
+    y, x = np.mgrid[0:height, 0:width]
+    return ((y // 8) * bx + x // 8) % world
 
 
 class FrameGather:
@@ -91,41 +99,44 @@ class FrameGather:
 
     # --- transports ------------------------------------------------------------
     def _open_ipc(self, required: bool) -> str:
-        """Every rank r > 0 exports its packed buffer, rank 0 maps them all and reads back a
-        probe word each rank wrote (r + 0.5 at slot 0): a transport that maps but delivers
-        nothing, or stale data, is caught here. Every rank must succeed (a MIN over the gloo
-        group), else all fall back to shm together."""
+        """Every rank r > 0 fills slot 0 of its packed buffer with r + 0.5 and exports it; rank 0
+        maps them all and pulls a whole probe frame through them with rt_shard_pull_unpack, the
+        kernel every gather runs (system-scope acquire and loads), checking that each block holds
+        its rank's value: a mapping that the kernel's loads cannot read, or that delivers nothing
+        or stale data, is caught here. The pull kernel takes at most 64 ranks. Every rank must
+        succeed (a MIN over the gloo group), else all fall back to shm together."""
         import torch
         import torch.distributed as dist
-        from . import copy_async, ipc_export, ipc_open
+        from . import ipc_export, ipc_open, shard_pull_unpack
         dev = self._dev()
-        ok = 1
+        ok = 1 if self.world <= MAX_PULL_RANKS else 0
         handle = None
-        if self.rank != 0:
+        if self.rank != 0 and ok:
             try:
-                self.d_pack[0].fill_(self.rank + 0.5)
+                self.d_pack[: max(self.cnt, 1)].fill_(self.rank + 0.5)
                 self._sync()
                 handle = ipc_export(self.d_pack.data_ptr(), dev)
             except Exception:
                 ok = 0
         handles = [None] * self.world
         dist.all_gather_object(handles, handle, group=self.group)
-        if self.rank == 0:
-            probe = torch.zeros(self.world, dtype=torch.float32, device=self.device)
+        if self.rank == 0 and ok:
             self._peers, self._peer_cnt = [0], [0]
             try:
                 for r in range(1, self.world):
                     cnt = shard_floats(self.w, self.h, r, self.world)
                     if handles[r] is None:
                         raise RuntimeError(f"rank {r} exported no buffer")
-                    ptr = ipc_open(handles[r], dev)
-                    self._peers.append(ptr)
+                    self._peers.append(ipc_open(handles[r], dev))
                     self._peer_cnt.append(max(cnt, 1))
-                    copy_async(probe.data_ptr() + 4 * r, ptr, 4, self._stream())
+                probe = torch.full((self.w * self.h * 3,), -1.0, dtype=torch.float32, device=self.device)
+                shard_pull_unpack(self._peers, self.w, self.h, probe, self._stream())
                 self._sync()
-                got = probe.cpu().tolist()
-                if any(got[r] != r + 0.5 for r in range(1, self.world)):
-                    raise RuntimeError(f"IPC probe read {got}")
+                want = torch.from_numpy(block_ranks(self.w, self.h, self.world).astype(np.float32) + 0.5)
+                want[want == 0.5] = -1.0  # rank 0's blocks are not pulled
+                got = probe.view(self.h * self.w, 3).cpu()
+                if not torch.equal(got, want.view(-1, 1).expand(-1, 3)):
+                    raise RuntimeError("IPC probe frame differs from the ranks' values")
             except Exception:
                 ok = 0
         flag = torch.tensor([ok], dtype=torch.int32)

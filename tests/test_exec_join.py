@@ -9,9 +9,12 @@ next in_unit_sphere() draw was wrong (C1 11834132 segments instead of 11882594).
 the allocator split there depended on unrelated code (SLP vectorization, dead blocks,
 debug stores), which is why it looked like never-executed code changing results.
 
-librtamd_rngdiv.so (make rngdiv) is kernel.hip built with the per-lane branch
-(RT_RNG_UNIFORM=0) under the product's flags: the regression fixture. The checker must
-find exactly those copies there and nothing in the product or the audit build.
+The checker's logic is pinned by two fixed disassembly excerpts (tests/golden/exec_join_*.s,
+cut by tests/golden/make_exec_join_snippets.py): the fixture's join with the two copies and a
+clean join of the product. __graft_entry__.build() runs the same check on the product and the
+audit build and fails on a hit. The live regression fixture (librtamd_rngdiv.so, make rngdiv:
+the out-of-line Philox call behind the per-lane branch) is only reported on: whether the
+allocator still splits there depends on the compiler and on unrelated code.
 """
 import os
 import sys
@@ -20,36 +23,67 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "tools"))
+sys.path.insert(0, ROOT)
 import exec_join_check as ejc  # noqa: E402
 import kernel_resources as kr  # noqa: E402
 
+import __graft_entry__ as ge  # noqa: E402
+
 LIB = os.path.join(ROOT, "raytracinginoneweekendinrust_amd", "_lib")
+GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 
-def test_product_has_no_vector_write_ahead_of_an_exec_restore():
-    found = ejc.check_library(kr.DEFAULT_LIB)
-    assert not found, [(kr.readable(f), hex(j), w) for f, j, w in found[:10]]
+def excerpt(name):
+    return open(os.path.join(GOLDEN, f"exec_join_{name}.s")).read()
 
 
-def test_audit_build_is_clean_too():
-    path = os.path.join(LIB, "librtamd_audit.so")
-    if not os.path.exists(path):
-        pytest.skip("audit build absent")
-    assert not ejc.check_library(path)
+def test_checker_finds_the_split_copies_in_the_golden_excerpt():
+    found = list(ejc.check_disassembly(excerpt("bad")))
+    assert [kr.readable(fn) for fn, _, _ in found] == ["trace_samples<0, 3, 1>"] * 2, found
+    assert len({j for _, j, _ in found}) == 1  # one join
+    ops = [w.split(": ", 1)[1] for _, _, w in found]
+    assert ops == ["v_mov_b32_e32 v4, v2", "v_mov_b32_e32 v5, v3"], ops
 
 
-def test_checker_finds_the_rng_buffer_copies_in_the_fixture():
+def test_checker_passes_a_join_that_restores_exec_first():
+    text = excerpt("good")
+    assert "s_and_saveexec_b64" in text and "s_or_b64 exec, exec" in text
+    assert not list(ejc.check_disassembly(text))
+
+
+def test_checker_flags_a_copy_moved_ahead_of_the_restore():
+    # the clean excerpt with a vector move put at the join label, ahead of its EXEC restore
+    # (the restore keeps its place in the text under an otherwise unused address)
+    lines = excerpt("good").splitlines()
+    ins = ejc.parse("\n".join(lines))
+    br = next(i for i, (_, _, mn, _) in enumerate(ins) if mn == "s_cbranch_execz")
+    join = ins[br][0] + 4 + 4 * int(ins[br][3].split()[0])
+    k = next(i for i, line in enumerate(lines) if f"// {join:012X}:" in line)
+    assert "s_or_b64 exec, exec" in lines[k]
+    moved = f"\tv_mov_b32_e32 v9, v8 // {join:012X}: 7E120308"
+    lines[k] = lines[k].replace(f"// {join:012X}:", f"// {join + 2:012X}:")
+    lines.insert(k, moved)
+    found = [w for _, j, w in ejc.check_disassembly("\n".join(lines)) if j == join]
+    assert found == [f"{join:#x}: v_mov_b32_e32 v9, v8"], found
+
+
+def test_build_guard_passes_the_product_and_the_audit_build():
+    paths = [kr.DEFAULT_LIB]
+    audit = os.path.join(LIB, "librtamd_audit.so")
+    if os.path.exists(audit):
+        paths.append(audit)
+    ge.exec_join_guard(paths)
+
+
+def test_build_guard_refuses_the_live_fixture_when_it_is_miscompiled():
     path = os.path.join(LIB, "librtamd_rngdiv.so")
     assert os.path.exists(path), "make -C raytracinginoneweekendinrust_amd/csrc rngdiv (__graft_entry__.build())"
     found = ejc.check_library(path)
-    per = {}
-    for fn, join, what in found:
-        per.setdefault(kr.readable(fn), []).append(what.split(": ", 1)[1])
-    # kernel.hip's instances that the fixture's allocator split that way: the C1 instance (which
-    # tests/test_gpu_exec_join.py renders) among them, two v_mov copies (r0, r2 of the buffer)
-    # at the join of the time draw's block fetch in each; which other instances show it moves
-    # with unrelated code (round 4: the triangle preset's, later the all-feature ones)
-    assert "trace_samples<0, 3, 1>" in per, per
-    for inst, ops in per.items():
-        assert inst.startswith("trace_samples<0,"), (inst, ops)
-        assert len(ops) == 2 and all(o.startswith("v_mov_b32") for o in ops), (inst, ops)
+    if not found:
+        pytest.skip("this compiler no longer splits the Rng buffer at the fixture's join (reported, not required)")
+    with pytest.raises(RuntimeError, match="EXEC-join miscompile"):
+        ge.exec_join_guard([path])
+    # whatever the allocator splits there is a plain copy into a register, in a fast-kernel instance
+    for fn, _, what in found:
+        assert kr.readable(fn).startswith("trace_samples<0,"), (fn, what)
+        assert what.split(": ", 1)[1].startswith("v_mov_b32"), what

@@ -65,19 +65,23 @@ def test_two_rank_bench_back_to_back_frames_over_both_transports():
         assert two["frame_md5"] == one["frame_md5"], transport
 
 
-@pytest.mark.parametrize("transport,world", [("ipc", 2), ("ipc", 3), ("shm", 2)])
-def test_frame_gather_position_coded_frames(transport, world, tmp_path):
+@pytest.mark.parametrize("transport,world,lag", [("ipc", 2, False), ("ipc", 3, False), ("shm", 2, False),
+                                                 ("ipc", 2, True), ("shm", 2, True)])
+def test_frame_gather_position_coded_frames(transport, world, lag, tmp_path):
     """FrameGather driven directly: 5 steps (both slots reused twice), a ragged 203 x 117
     frame whose every float is distinct and changes each step; rank 0's frame must equal
-    it bit for bit after every step (tests/gather_worker.py)."""
+    it bit for bit after every step (tests/gather_worker.py). `lag`: rank 0's pulls run ~20 ms
+    late on its GPU and it never synchronises inside the loop, so the peers run ahead and the
+    two-slot reuse rule is what keeps a peer from overwriting a slot still being read."""
     out = tmp_path / "gather.json"
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
                         "--master-addr", "127.0.0.1", "--master-port", str(_port()),
-                        os.path.join(ROOT, "tests", "gather_worker.py"), transport, "203", "117", "5", str(out)],
+                        os.path.join(ROOT, "tests", "gather_worker.py"), transport, "203", "117", "5", str(out),
+                        *(["lag"] if lag else [])],
                        capture_output=True, text=True, env=env, timeout=240, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     res = json.loads(out.read_text())
-    assert res["transport"] == transport and res["world"] == world
+    assert res["transport"] == transport and res["world"] == world and res["lag"] == lag
     assert len(res["steps"]) == 5
     assert all(st["equal"] for st in res["steps"]), res["steps"]

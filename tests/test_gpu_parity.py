@@ -282,11 +282,17 @@ def test_full_workload_subsample_matches_oracle(cfg_name, shard, rt, orc):
     sub = rt.render_params(cfg.width, cfg.height, cfg.spp, cfg.depth, background=cfg.background(),
                            shard_index=shard, shard_count=256)
     want = np.full_like(got, np.nan)
-    orc.render(scene, cfg.camera(), sub, out=want)
+    _, cnt = orc.render(scene, cfg.camera(), sub, out=want)
     mask = ~np.isnan(want[..., 0])
     assert mask.sum() > 3000
     np.testing.assert_array_equal(got[mask], want[mask])
     assert np.isfinite(got).all()
+    # the same shard rendered alone on the GPU: its pixels and its segment count (a draw-count
+    # drift that left the shard's pixels unchanged would still move the count)
+    shard, st_sh = gpu_render(rt, scene, cfg.camera(), sub)
+    np.testing.assert_array_equal(shard[mask], want[mask])
+    assert st_sh["samples"] == int(mask.sum()) * cfg.spp
+    assert st_sh["segments"] == cnt["segments"], (st_sh["segments"], cnt["segments"])
 
 
 def test_c1_full_frame_matches_oracle(rt, orc):
@@ -421,13 +427,15 @@ def test_replay_pass_kernels_match_oracle(cfg_name, w, h, replay_ref, rt, orc):
 
 
 @pytest.mark.parametrize("stream", [True, False])
-@pytest.mark.parametrize("cfg_name", ["C3", "C5"])
+@pytest.mark.parametrize("cfg_name", ["C3", "C5", "C4"])
 def test_streaming_replay_pass_matches_oracle(cfg_name, stream, rt, orc):
     # The streaming replay pass (kernel.hip replay_claim) runs beside the fast kernel and takes
     # the handed-over samples while the fast kernel drains; RT_OPT_TUNE bit 17 leaves them all
     # to the serialized pass. A 4096 x 1 image (v = j / (H - 1) = NaN: every ray is handed
     # over) with 8 spp gives 4096 work units, enough to fill the GPU, so the fast kernel's
     # waves drain while the stream's waves wait for slots, and every sample is replayed.
+    # C4 is the deep-stack case: its replay runs trace_samples<3, 3, kFAll> and the streaming
+    # waves spill into their own slabs behind the fast kernel's (the grid + kStreamWaves layout).
     cfg = rt.CONFIGS[cfg_name]
     scene = rt.Scene.generate(cfg.scene, cfg.scene_seed)
     w, h, spp = 4096, 1, 8

@@ -86,13 +86,22 @@ def parse(dis: str):
     return out
 
 
-def check_code_object(co: bytes):
-    """Yields (function, join address, offending instruction) for one code object."""
+def disassemble(co: bytes) -> str:
     with tempfile.NamedTemporaryFile(suffix=".co") as f:
         f.write(co)
         f.flush()
-        dis = subprocess.run([OBJDUMP, "-d", "--no-show-raw-insn", "--mcpu=gfx950", f.name], capture_output=True,
-                             text=True, check=True).stdout
+        return subprocess.run([OBJDUMP, "-d", "--no-show-raw-insn", "--mcpu=gfx950", f.name], capture_output=True,
+                              text=True, check=True).stdout
+
+
+def check_code_object(co: bytes):
+    """Yields (function, join address, offending instruction) for one code object."""
+    yield from check_disassembly(disassemble(co))
+
+
+def check_disassembly(dis: str):
+    """Yields (function, join address, offending instruction) for llvm-objdump -d text
+    (tests/golden/exec_join_*.s hold excerpts with and without the split copies)."""
     ins = parse(dis)
     index = {a: i for i, (a, _, _, _) in enumerate(ins)}
     starts = []
