@@ -309,6 +309,10 @@ int rt_bvh_build_order(const float* d_keys, uint32_t n, uint64_t seed, uint32_t*
  *                           (default), 1 = host always, 2 = device always
  *   RT_OPT_GUIDE            guided batch divisor K: a batch is at most (units left) /
  *                           (K x waves) units (1..256; 0 = the default 2)
+ *   RT_OPT_MIGRATE          drain hand-over: once the work pool is dry, a fast-kernel wave with
+ *                           at most this many paths left hands them to the streaming replay
+ *                           pass, which resumes them packed into full waves (0..64; 0 = off;
+ *                           -1 = the default 16)
  * Returns RT_ERR_INVALID for an unknown option or a value out of range. */
 typedef enum {
     RT_OPT_TUNE = 0,
@@ -319,7 +323,8 @@ typedef enum {
     RT_OPT_LAUNCH_LOG = 5,
     RT_OPT_BVH_BUILD = 6,
     RT_OPT_GUIDE = 7,
-    RT_OPT_COUNT = 8
+    RT_OPT_MIGRATE = 8,
+    RT_OPT_COUNT = 9
 } rt_option;
 int rt_set_option(int option, int64_t value);
 int rt_get_option(int option, int64_t* value);

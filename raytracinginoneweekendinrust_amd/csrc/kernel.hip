@@ -1162,9 +1162,236 @@ RT_DEV bool bvh_hit(const DevScene& S, float delta, uint32_t root, const Ray& r,
 // false; the walk resumes it on a later trip of the sample loop, together with the lanes
 // that reach the same BVH then. The visit order and every value are unchanged, only when a
 // visit runs differs, so the result is the same bits.
+#ifndef RT_EXP_TRIP
+#define RT_EXP_TRIP 1
+#endif
+// The fast BVH4 traversal without leaf postponement (every preset but the triangle one, and the
+// replay pass): one node per trip; a leaf node's 1-2 leaves are tested at once, an interior
+// node's four slots get the packed box test, the sort network and the pushes only on the
+// interior branch (a leaf trip goes straight to the pop), and a pop reads an entry's node and
+// key together. Same visits, same candidates, same merge as bvh_run's general loop.
+template <int kKind, uint32_t kF>
+RT_DEV void bvh_run_immediate(const DevScene& S, float delta, const f4* wrapper, const Ray& r, V inv, float tmin,
+                              float& closest, uint32_t& hit_code, uint32_t* stk, uint32_t mode, Trav& tv) {
+    const float tmax_entry = tv.tmax_entry;
+    const bool prune = (__float_as_uint(wrapper[7].w) & rtdev::kBvhPrunable) != 0u || (mode & kModePruneAllExp);
+    const float dmi = delta * fmaxf(fmaxf(__builtin_fabsf(inv.x), __builtin_fabsf(inv.y)), __builtin_fabsf(inv.z));
+    const bool leaf_boxes = prune && !(mode & kModeNoLeafBoxes);
+    [[maybe_unused]] const uint32_t hnx = inv.x < 0.0f ? 48u : 0u, hny = inv.y < 0.0f ? 64u : 16u,
+                                    hnz = inv.z < 0.0f ? 80u : 32u;
+    bool any = tv.any;
+    uint32_t best_rank = tv.best_rank, sp = tv.sp, cur = tv.cur;
+#ifdef RT_PROFILE_REGIONS
+    uint32_t visits = 0;
+#endif
+    for (;;) {
+        uint32_t onx, ony, onz;  // near-plane row offsets (bvh_run)
+        if constexpr ((kF & kFTri) != 0u) {
+            onx = hnx;
+            ony = hny;
+            onz = hnz;
+        } else {
+            uint32_t msx, msy, msz;
+            asm volatile("v_ashrrev_i32 %0, 31, %1" : "=v"(msx) : "v"(inv.x));
+            asm volatile("v_ashrrev_i32 %0, 31, %1" : "=v"(msy) : "v"(inv.y));
+            asm volatile("v_ashrrev_i32 %0, 31, %1" : "=v"(msz) : "v"(inv.z));
+            onx = msx & 48u;
+            ony = (msy & 48u) + 16u;
+            onz = (msz & 48u) + 32u;
+        }
+#ifdef RT_LEAF_AUDIT
+        if ((cur & ~rtdev::kLeafNodeFlag) >= S.num_nodes || sp > S.stack_depth + S.spill_depth) {
+            atomicAdd(&g_bounds_audit_count, 1u);
+            break;
+        }
+#endif
+#ifdef RT_PROFILE_REGIONS
+        ++visits;
+#endif
+        PROF_T0(pt);
+        if ((cur & rtdev::kLeafNodeFlag) != 0u) {
+            // the 1-2 leaves of one reference BVH2 node, formed like bvh.rs:377-414 (bvh_run)
+            const uint32_t nbo = (cur & ~rtdev::kLeafNodeFlag) * (rtdev::kBvhNodeF4 * 16u);
+            const f4* nd = S.nodes;
+            const float2 nx2 = ld2_at(nd, nbo + onx), ny2 = ld2_at(nd, nbo + ony), nz2 = ld2_at(nd, nbo + onz),
+                         fx2 = ld2_at(nd, nbo + (onx ^ 48u)), fy2 = ld2_at(nd, nbo + (ony ^ 80u)),
+                         fz2 = ld2_at(nd, nbo + (onz ^ 112u)), chs = ld2_at(nd, nbo + 96u), rks = ld2_at(nd, nbo + 112u);
+            float tmr = tmax_entry, nt = 0.0f;
+            bool nh = false;
+            uint32_t ncode = 0u, nrank = 0u;
+            const uint32_t nleaf = __float_as_uint(chs.y) == rtdev::kChildEmpty ? 1u : 2u;
+            float llo[2] = {-kInf, -kInf}, lhi[2] = {kInf, kInf};
+            if (leaf_boxes) leaf_intervals2_nf(nx2, ny2, nz2, fx2, fy2, fz2, r, inv, delta, llo, lhi);
+            for (uint32_t k = 0; k < nleaf; ++k) {
+                const uint32_t lcode = __float_as_uint(k ? chs.y : chs.x), rank = __float_as_uint(k ? rks.y : rks.x);
+#ifdef RT_LEAF_AUDIT
+                const float2 bx0 = ld2(S.nodes + nbo / 16u, 0), by0 = ld2(S.nodes + nbo / 16u, 1),
+                             bz0 = ld2(S.nodes + nbo / 16u, 2), bx1 = ld2(S.nodes + nbo / 16u, 3),
+                             by1 = ld2(S.nodes + nbo / 16u, 4), bz1 = ld2(S.nodes + nbo / 16u, 5);
+                const float x0 = k ? bx0.y : bx0.x, y0 = k ? by0.y : by0.x, z0 = k ? bz0.y : bz0.x;
+                const float x1 = k ? bx1.y : bx1.x, y1 = k ? by1.y : by1.x, z1 = k ? bz1.y : bz1.x;
+#endif
+                const float bound = tmr < closest ? tmr : closest;
+                if (!leaf_boxes || leaf_interval_may_hit(k ? llo[1] : llo[0], k ? lhi[1] : lhi[0], tmin, bound)) {
+                    PROF_T0(pl);
+                    const float cap = closest < kInf ? __uint_as_float(__float_as_uint(closest) + 1u) : kInf;
+                    float c = tmr < cap ? tmr : cap;
+                    uint32_t code = 0u;
+                    const RayD q = to_d(r);
+                    if (leaf_hit<kF>(S, lcode, r, q, tmin, c, code)) {
+                        const uint32_t rk = rank + (rtdev::leaf_type(lcode) == rtdev::kLeafCube
+                                                        ? rtdev::leaf_index(code) - rtdev::leaf_index(lcode)
+                                                        : 0u);
+                        if (!nh || !(nt < c)) {
+                            nh = true;
+                            nt = c;
+                            ncode = code;
+                            nrank = rk;
+                        }
+                        tmr = c;
+                    }
+                    PROF_ADD(kPrLeafTest, pl);
+                } else {
+                    LEAF_AUDIT(lcode, rank, x0, y0, z0, x1, y1, z1);
+                }
+            }
+            if (nh && (nt < closest || (nt == closest && nrank > best_rank))) {
+                closest = nt;
+                best_rank = nrank;
+                hit_code = ncode;
+                any = true;
+            }
+            PROF_ADD(kPrBvhTrip, pt);
+        } else {
+            const uint32_t nbo = cur * (rtdev::kBvhNodeF4 * 16u);
+            const f4* nd = S.nodes;
+            const f4 nx = ld4_at(nd, nbo + onx), ny = ld4_at(nd, nbo + ony), nz = ld4_at(nd, nbo + onz),
+                     fx = ld4_at(nd, nbo + (onx ^ 48u)), fy = ld4_at(nd, nbo + (ony ^ 80u)),
+                     fz = ld4_at(nd, nbo + (onz ^ 112u)), chf = ld4_at(nd, nbo + 96u);
+            uint32_t c0 = __float_as_uint(chf.x), c1 = __float_as_uint(chf.y), c2 = __float_as_uint(chf.z),
+                     c3 = __float_as_uint(chf.w);
+            float key[4];
+            child_keys4_nf(nx, ny, nz, fx, fy, fz, r, inv, tmin, tmax_entry, prune ? prune_bound(closest) : kInf,
+                           prune ? dmi : 0.0f, key);
+            float t0 = key[0], t1 = key[1], t2 = key[2], t3 = key[3];
+            PROF_ADD(kPrBvhTrip, pt);
+            PROF_T0(pp);
+#if defined(RT_EXP_NOSORT) && RT_EXP_NOSORT
+            // EXPERIMENT (A/B only): no sort network. Slots in DFS order (1), or reversed when the
+            // ray runs against the node's top split axis (2, the axis in the rank row's low bits);
+            // the first passing slot is visited next and the others pushed in reverse, so the
+            // order approximates near-first. Same visit set, same merge: the same bits.
+            if (RT_EXP_NOSORT == 2) {
+                const uint32_t ax = __float_as_uint(ld2_at(nd, nbo + 112u).x) & 3u;
+                const float dax = ax == 0u ? r.d.x : (ax == 1u ? r.d.y : r.d.z);
+                if (dax < 0.0f) {
+                    float tt = t0; t0 = t3; t3 = tt; tt = t1; t1 = t2; t2 = tt;
+                    uint32_t cc = c0; c0 = c3; c3 = cc; cc = c1; c1 = c2; c2 = cc;
+                }
+            }
+            {
+                const bool v0 = t0 != kInf, v1 = t1 != kInf, v2 = t2 != kInf, v3 = t3 != kInf;
+                if (v0 || v1 || v2 || v3) {
+                    auto push = [&](uint32_t node, float t) {
+                        if (!(kF & kFDeep) || sp < S.stack_depth) {
+                            stk[sp * 128u] = node;
+                            stk[sp * 128u + 64u] = __float_as_uint(t);
+                        } else {
+                            uint32_t* g = S.stack_spill +
+                                          (((size_t)blockIdx.x * S.spill_depth + (sp - S.stack_depth)) * 64u + threadIdx.x) * 2u;
+                            g[0] = node;
+                            g[1] = __float_as_uint(t);
+                        }
+                        sp += 1u;
+                    };
+                    if (v3 && (v0 || v1 || v2)) push(c3, t3);
+                    if (v2 && (v0 || v1)) push(c2, t2);
+                    if (v1 && v0) push(c1, t1);
+                    cur = v0 ? c0 : (v1 ? c1 : (v2 ? c2 : c3));
+                    PROF_ADD(kPrBvhPush, pp);
+                    continue;
+                }
+            }
+#else
+            sort2(t0, c0, t1, c1);
+            sort2(t2, c2, t3, c3);
+            sort2(t0, c0, t2, c2);
+            sort2(t1, c1, t3, c3);
+            sort2(t1, c1, t2, c2);
+#endif
+            if (t0 != kInf) {  // visit the nearest next, push the others far to near
+                auto push = [&](uint32_t node, float t) {
+                    if (!(kF & kFDeep) || sp < S.stack_depth) {
+                        stk[sp * 128u] = node;
+                        stk[sp * 128u + 64u] = __float_as_uint(t);
+                    } else {
+                        uint32_t* g = S.stack_spill +
+                                      (((size_t)blockIdx.x * S.spill_depth + (sp - S.stack_depth)) * 64u + threadIdx.x) * 2u;
+                        g[0] = node;
+                        g[1] = __float_as_uint(t);
+                    }
+                    sp += 1u;
+                };
+                if (t3 != kInf) push(c3, t3);
+                if (t2 != kInf) push(c2, t2);
+                if (t1 != kInf) push(c1, t1);
+                cur = c0;
+                PROF_ADD(kPrBvhPush, pp);
+                continue;
+            }
+            PROF_ADD(kPrBvhPush, pp);
+        }
+        PROF_T0(ppop);
+        // pop the nearest-pushed entry whose key the current bound does not prune
+        const float pb = prune ? prune_bound(closest) : kInf;
+        bool found = false;
+        while (sp > 0u) {
+            sp -= 1u;
+            uint32_t cand, tb;
+            if (!(kF & kFDeep) || sp < S.stack_depth) {
+                cand = stk[sp * 128u];
+                tb = stk[sp * 128u + 64u];
+            } else {
+                const uint32_t* g = S.stack_spill +
+                                    (((size_t)blockIdx.x * S.spill_depth + (sp - S.stack_depth)) * 64u + threadIdx.x) * 2u;
+                cand = g[0];
+                tb = g[1];
+            }
+            if (!(__uint_as_float(tb) > pb)) {
+                cur = cand;
+                found = true;
+                break;
+            }
+        }
+        PROF_ADD(kPrBvhPop, ppop);
+        if (!found) break;
+    }
+    tv = Trav{cur, sp, best_rank, tmax_entry, any, kNoNode};
+#ifdef RT_PROFILE_REGIONS
+    {
+        const uint32_t b = trips_bin(visits);
+        uint32_t m = visits;
+        for (int off = 32; off > 0; off >>= 1) {
+            uint32_t o = __shfl_xor(m, off);
+            m = o > m ? o : m;
+        }
+        const uint32_t first = (uint32_t)__builtin_ctzll(__ballot(1));
+        for (uint32_t bin = 0; bin < 8u; ++bin) {
+            const uint32_t n = (uint32_t)__popcll(__ballot(b == bin));
+            if (__lane_id() == first && n) prof_lds[3u * kPrCount + bin] += n;
+        }
+        if (__lane_id() == first) prof_lds[3u * kPrCount + 8u + trips_bin(m)] += 1u;
+    }
+#endif
+}
+
 template <int kKind, uint32_t kF, bool kSusp>
 RT_DEV bool bvh_run(const DevScene& S, float delta, const f4* wrapper, const Ray& r, V inv, float tmin, float& closest,
                     uint32_t& hit_code, uint32_t* stk, uint32_t mode, Trav& tv, uint32_t susp) {
+    if constexpr (RT_EXP_TRIP && !kSusp && !((kF & kFTri) != 0u && kKind == 0)) {
+        bvh_run_immediate<kKind, kF>(S, delta, wrapper, r, inv, tmin, closest, hit_code, stk, mode, tv);
+        return true;
+    }
     const float tmax_entry = tv.tmax_entry;
     const bool prune = (__float_as_uint(wrapper[7].w) & rtdev::kBvhPrunable) != 0u || (mode & kModePruneAllExp);
     const float dmi = delta * fmaxf(fmaxf(__builtin_fabsf(inv.x), __builtin_fabsf(inv.y)), __builtin_fabsf(inv.z));
@@ -1486,6 +1713,9 @@ RT_DEV void spheres_surely_missed2(f4 s0, f4 s1, const Ray& r, float a, bool& m0
     m1 = m[1] > 0x1p-100f && disc[1] < lim[1];
 }
 
+#ifndef RT_EXP_UNIFORM_RECT
+#define RT_EXP_UNIFORM_RECT 1
+#endif
 constexpr uint32_t kRunPretestMin = 8u;  // sphere runs at least this long take the f32 pretest
 // A GEOM or BVH entry (the caller guarantees E is wave-uniform). Only instances
 // with kFRuns carry the f32 pretest of long sphere runs, only those with kFBvh the
@@ -1541,6 +1771,32 @@ RT_DEV bool entry_geom_hit(const DevScene& S, float delta, const DevEntry* E, Ra
             return bvh_hit<kKind, kF>(S, delta, E->payload, r, tmin, closest, hit_code, stk, mode, replay);
         }
     }
+#if RT_EXP_UNIFORM_RECT
+    {
+        // A top-level rectangle (walls, lights): its record is the same for the whole wave, so its
+        // plane axis is read once (readfirstlane) and the wave branches on it, instead of every lane
+        // selecting the six ray components per axis (rect_axes). Same operations as rect_t.
+        const uint32_t code = __builtin_amdgcn_readfirstlane(E->payload);
+        if (rtdev::leaf_type(code) == rtdev::kLeafRect) {
+            const uint32_t idx = rtdev::leaf_index(code);
+            const f4 r0 = ld4(S.rect + 2 * idx), r1 = ld4(S.rect + 2 * idx + 1);
+            const uint32_t axis = __builtin_amdgcn_readfirstlane(__float_as_uint(r1.y));
+            float t;
+            bool h;
+            if (axis == 0u)  // XY: plane z
+                h = side_t(r0.x, r.o.z, r.d.z, r.o.x, r.d.x, r.o.y, r.d.y, r0.y, r0.z, r0.w, r1.x, tmin, closest, t);
+            else if (axis == 1u)  // XZ: plane y
+                h = side_t(r0.x, r.o.y, r.d.y, r.o.x, r.d.x, r.o.z, r.d.z, r0.y, r0.z, r0.w, r1.x, tmin, closest, t);
+            else  // YZ: plane x
+                h = side_t(r0.x, r.o.x, r.d.x, r.o.y, r.d.y, r.o.z, r.d.z, r0.y, r0.z, r0.w, r1.x, tmin, closest, t);
+            if (h) {
+                closest = t;
+                hit_code = code;
+            }
+            return h;
+        }
+    }
+#endif
     RayD q = to_d(r);
     ABLATE(kAbGeom2, float c2 = closest; uint32_t h2 = 0u;
            if (leaf_hit<kF | kFLeafRM>(S, E->payload, r, q, tmin, c2, h2) && h2 == 0x7fffffffu) closest = -1.0f;);
@@ -2052,6 +2308,7 @@ struct ChunkParams {
     uint32_t nslots;          // sample-buffer plane size: 64 slots per 8x8 block of the shard, block-major
     uint32_t group;           // units per batch at most (batch_group)
     uint32_t blocks;          // 8x8 blocks of the shard (units = blocks x samples)
+    uint32_t migrate;         // drain hand-over: a dry wave with at most this many paths left hands them over (0: off)
 };
 
 // HittableList::hit over the world (hittable.rs:100-118), t in [0.001, inf).
@@ -2180,6 +2437,7 @@ struct TraceCounters {
     unsigned fast_done;          // fast-kernel waves that have finished (the streaming replay's end)
     unsigned stream_abort;       // the streaming replay gave up a claimed entry: re-render the chunk
     unsigned long long fast_segments;  // segments of the fast kernel's and streaming replay's samples
+    unsigned migrate_count;      // path records the fast kernel's draining waves handed over (below)
 };
 // A replay-list entry: the sample's pixel and its chunk-local sample index. Entries are
 // written and read as one 64-bit agent-scope atomic: the streaming replay pass reads them
@@ -2206,6 +2464,44 @@ RT_DEV ReplayItem replay_take(const ReplayItem* list, uint32_t idx) {
     return ReplayItem{(uint32_t)v, (uint32_t)(v >> 32)};
 }
 constexpr uint32_t kReplayCap = 1u << 20;
+// The drain hand-over. Once the work pool is dry, a fast-kernel wave with at most Q.migrate
+// paths still running writes each path's whole state (PathRecord) behind the replay list and
+// publishes it as a replay entry flagged kMigrated, then exits. The streaming replay pass, which
+// takes the slots the fast kernel's waves leave, resumes those paths where they stopped, packed
+// into full waves: the last long paths of a launch run in few waves instead of one or two lanes
+// of many waves that share every SIMD's issue slots. A path continues from the same state with
+// the same Philox stream, so its result and segment count are the ones it would have had.
+constexpr uint32_t kMigrateCap = 1u << 16;
+constexpr uint32_t kMigrated = 0x80000000u;  // ReplayItem.sample flag: .pixel is a path record index
+#ifndef RT_MIGRATE_DEFAULT
+#define RT_MIGRATE_DEFAULT 16
+#endif
+constexpr uint32_t kMigrateDefault = RT_MIGRATE_DEFAULT;  // rt_set_option(RT_OPT_MIGRATE, -1)
+constexpr uint32_t kPathRecordU4 = 6u;  // a path record: 6 x 16 B behind the replay list
+RT_DEV uint4* path_records(const ReplayItem* list) {
+    return reinterpret_cast<uint4*>(const_cast<ReplayItem*>(list) + kReplayCap);
+}
+RT_DEV void save_path(uint4* rec, uint32_t slot, uint32_t s_local, uint32_t depth, const Rng& g, V L, V T,
+                      const Ray& ray) {
+    rec[0] = make_uint4(slot, s_local, depth, g.sample);
+    rec[1] = make_uint4(g.pixel, g.d, g.r0, g.r1);
+    rec[2] = make_uint4(g.r2, __float_as_uint(L.x), __float_as_uint(L.y), __float_as_uint(L.z));
+    rec[3] = make_uint4(__float_as_uint(T.x), __float_as_uint(T.y), __float_as_uint(T.z), __float_as_uint(ray.time));
+    rec[4] = make_uint4(__float_as_uint(ray.o.x), __float_as_uint(ray.o.y), __float_as_uint(ray.o.z),
+                        __float_as_uint(ray.d.x));
+    rec[5] = make_uint4(__float_as_uint(ray.d.y), __float_as_uint(ray.d.z), 0u, 0u);
+}
+RT_DEV void load_path(const uint4* rec, uint32_t& slot, uint32_t& s_local, uint32_t& depth, Rng& g, V& L, V& T,
+                      Ray& ray) {
+    const uint4 a = rec[0], b = rec[1], c = rec[2], d = rec[3], e = rec[4], f = rec[5];
+    slot = a.x; s_local = a.y; depth = a.z; g.sample = a.w;
+    g.pixel = b.x; g.d = b.y; g.r0 = b.z; g.r1 = b.w;
+    g.r2 = c.x; L = mk(__uint_as_float(c.y), __uint_as_float(c.z), __uint_as_float(c.w));
+    T = mk(__uint_as_float(d.x), __uint_as_float(d.y), __uint_as_float(d.z));
+    ray.time = __uint_as_float(d.w);
+    ray.o = mk(__uint_as_float(e.x), __uint_as_float(e.y), __uint_as_float(e.z));
+    ray.d = mk(__uint_as_float(e.w), __uint_as_float(f.x), __uint_as_float(f.y));
+}
 // The streaming replay pass (trace_samples<3> with fixup 2, on a second stream) claims
 // entries one at a time while the fast kernel drains. Returns the claimed entry's index once
 // it is published, or kReplayNone when the fast kernel finished without one, the list
@@ -2213,6 +2509,34 @@ constexpr uint32_t kReplayCap = 1u << 20;
 constexpr uint32_t kReplayNone = 0xffffffffu;
 constexpr uint32_t kStreamWaves = 512;  // waves of the streaming replay pass
 constexpr unsigned long long kStreamTimeoutTicks = 1000000000ull;  // 10 s of s_memrealtime (100 MHz)
+// With the drain hand-over on (Q.migrate), one claim takes `cnt` consecutive entries and waits until
+// every one of them is published, or until the fast kernel has finished without producing the
+// last ones (cnt then shrinks to the entries that exist: none is lost, the count is final).
+RT_DEV uint32_t replay_claim_n(TraceCounters* ctr, const ReplayItem* list, uint32_t fast_grid, uint32_t& cnt) {
+    const uint32_t i = atomicAdd(&ctr->replay_pull, cnt);
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+        const bool done = __hip_atomic_load(&ctr->fast_done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) >= fast_grid;
+        const uint32_t n = __hip_atomic_load(&ctr->replay_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (i >= kReplayCap) return kReplayNone;
+        if (done || n >= i + cnt) {
+            uint32_t e = i + cnt < n ? i + cnt : n;
+            e = e < kReplayCap ? e : kReplayCap;
+            if (e <= i) return kReplayNone;
+            uint32_t j = i;
+            while (j < e && replay_peek(list, j) != kReplayFree) ++j;
+            if (j == e) {
+                cnt = e - i;
+                return i;
+            }
+        }
+        if (__builtin_amdgcn_s_memrealtime() - t0 > kStreamTimeoutTicks) {
+            atomicExch(&ctr->stream_abort, 1u);
+            return kReplayNone;
+        }
+        __builtin_amdgcn_s_sleep(64);  // items arrive in bursts while the waves drain
+    }
+}
 RT_DEV uint32_t replay_claim(TraceCounters* ctr, const ReplayItem* list, uint32_t fast_grid) {
     const uint32_t i = atomicAdd(&ctr->replay_pull, 1u);
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
@@ -2269,8 +2593,8 @@ RT_DEV bool take_sample(ItemPool& pool, bool want, const DevCamera& C, const Dev
                 // The streaming replay keeps 1 + backlog / waves lanes of a wave busy: the
                 // replayed paths are few and long, and a wave's segment takes as long as its
                 // slowest lane, so they spread over the waves unless there are many.
-                uint32_t lim = 1u;
-                if (leader) {
+                uint32_t lim = Q.migrate ? 64u : 1u;  // handed-over paths are packed (kMigrateCap)
+                if (leader && !Q.migrate) {
                     const uint32_t n = __hip_atomic_load(&ctr->replay_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     const uint32_t pl = __hip_atomic_load(&ctr->replay_pull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     lim += (n > pl ? n - pl : 0u) / gridDim.x;
@@ -2279,7 +2603,17 @@ RT_DEV bool take_sample(ItemPool& pool, bool want, const DevCamera& C, const Dev
                 if (64u - (uint32_t)__popcll(need) >= lim) break;
             }
             if (leader) {
-                if (list && stream_grid) {  // the streaming replay: one entry per claim
+                if (list && stream_grid && Q.migrate) {  // as many entries as idle lanes, or the backlog
+                    const uint32_t n = __hip_atomic_load(&ctr->replay_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const uint32_t pl = __hip_atomic_load(&ctr->replay_pull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const uint32_t backlog = n > pl ? n - pl : 0u, idle = (uint32_t)__popcll(need);
+                    cnt = backlog < idle ? backlog : idle;
+                    cnt = cnt < 1u ? 1u : cnt;
+                    bt = replay_claim_n(ctr, list, stream_grid, cnt);
+#ifdef RT_PROFILE_REGIONS
+                    role_event(bt);
+#endif
+                } else if (list && stream_grid) {  // the streaming replay: one entry per claim
                     cnt = 1u;
                     bt = replay_claim(ctr, list, stream_grid);
 #ifdef RT_PROFILE_REGIONS
@@ -2314,11 +2648,21 @@ RT_DEV bool take_sample(ItemPool& pool, bool want, const DevCamera& C, const Dev
             uint32_t x, y, s, sl;
             if (list) {
                 const ReplayItem it = replay_take(list, pool.next + rank);
-                y = it.pixel / P.width;
-                x = it.pixel - y * P.width;
-                s = it.sample;
-                const uint32_t blk = (y >> 3) * P.blocks_x + (x >> 3);
-                sl = ((blk - P.shard_index) / P.shard_count) * 64u + ((y & 7u) << 3) + (x & 7u);
+                if (it.sample & kMigrated) {
+                    // a path a draining fast-kernel wave handed over: it continues where it stopped
+                    // (the record was written before the entry was published, behind a release)
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                    load_path(path_records(list) + (size_t)it.pixel * kPathRecordU4, slot, s_local, depth, g, L, T, ray);
+                    got = true;
+                    x = P.width;  // nothing to start below
+                    y = s = sl = 0u;
+                } else {
+                    y = it.pixel / P.width;
+                    x = it.pixel - y * P.width;
+                    s = it.sample;
+                    const uint32_t blk = (y >> 3) * P.blocks_x + (x >> 3);
+                    sl = ((blk - P.shard_index) / P.shard_count) * 64u + ((y & 7u) << 3) + (x & 7u);
+                }
             } else {
                 // unit pool.batch + (item >> 6); a batch (<= Q.group <= Q.samples units) crosses at
                 // most one block boundary, so the batch's block and sample are divided once
@@ -2639,6 +2983,40 @@ __global__ __launch_bounds__(64, kWaves) void trace_samples(DevScene Sg, DevCame
         }
         PROF_ADD(kPrRefill, pr);
         if (__ballot(has) == 0ull) break;  // pool exhausted and every path finished
+        if constexpr (kKind == 0) {
+            // The drain hand-over (kMigrateCap above): the pool is dry and few of this wave's
+            // paths are left, so they move to the streaming replay pass and the wave exits.
+            if (Q.migrate && pool.exhausted) {
+                const unsigned long long act = __ballot(has);
+                const uint32_t nact = (uint32_t)__popcll(act);
+                if (nact <= Q.migrate) {
+                    uint32_t mbase = kReplayNone, rbase = 0u;
+                    if (lane == 0u) {  // the whole wave is here (uniform control flow)
+                        mbase = atomicAdd(&ctr->migrate_count, nact);
+                        if (mbase + nact <= kMigrateCap)
+                            rbase = atomicAdd(&ctr->replay_count, nact);
+                        else
+                            mbase = kReplayNone;
+                    }
+                    mbase = __builtin_amdgcn_readfirstlane(mbase);
+                    rbase = __builtin_amdgcn_readfirstlane(rbase);
+                    // (a replay list that overflows is re-rendered whole by the serialized pass,
+                    // so lanes that could not publish just go on)
+                    if (mbase != kReplayNone && rbase + nact <= kReplayCap) {
+                        if (has) {
+                            const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32),
+                                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
+                            save_path(path_records(replay_list) + (size_t)(mbase + r) * kPathRecordU4, slot,
+                                      take_sample_idx, depth, g, L, T, ray);
+                            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                            replay_publish(replay_list, rbase + r, mbase + r, kMigrated | take_sample_idx);
+                            has = false;
+                        }
+                        break;
+                    }
+                }
+            }
+        }
 #ifdef RT_PROFILE_REGIONS
         if (kKind == 0) {  // throughput histogram: this iteration's segments into the current bucket
             const uint32_t b = (uint32_t)((__builtin_amdgcn_s_memrealtime() - wave_t0) / kTpTicks);
@@ -2962,7 +3340,7 @@ TraceKernel fast_instance(int waves, uint32_t features) {
 }
 
 // rt_set_option's process-wide diagnostic switches (include/rt.h rt_option).
-std::atomic<int64_t> g_opt[RT_OPT_COUNT] = {{0}, {0}, {0}, {0}, {-1}, {0}, {0}, {0}};
+std::atomic<int64_t> g_opt[RT_OPT_COUNT] = {{0}, {0}, {0}, {0}, {-1}, {0}, {0}, {0}, {-1}};
 int64_t opt(int o) { return g_opt[o].load(std::memory_order_relaxed); }
 
 int check_device(int device) {
@@ -3408,7 +3786,9 @@ int rt_render_launch_camera(rt_scene_handle s, const rt_camera* camera, const rt
             return rthost::set_error(RT_ERR_OOM, std::string("hipMalloc counter: ") + hipGetErrorString(e));
     }
     if (!s->replay) {
-        if ((e = hipMalloc(&s->replay, sizeof(ReplayItem) * (size_t)kReplayCap)) != hipSuccess)
+        // the list, then the drain hand-over's path records (kMigrateCap x 96 B)
+        if ((e = hipMalloc(&s->replay, sizeof(ReplayItem) * (size_t)kReplayCap +
+                                           sizeof(uint4) * kPathRecordU4 * (size_t)kMigrateCap)) != hipSuccess)
             return rthost::set_error(RT_ERR_OOM, std::string("hipMalloc replay list: ") + hipGetErrorString(e));
         if ((e = hipMemsetAsync(s->replay, 0xff, sizeof(ReplayItem) * (size_t)kReplayCap, (hipStream_t)stream)) !=
             hipSuccess)  // every entry kReplayFree
@@ -3512,6 +3892,13 @@ int rt_render_launch_camera(rt_scene_handle s, const rt_camera* camera, const rt
         q.guide = 2u;  // measured on C3 (63 and 500 spp): 2 beats 4, 8, 16 and 32 (tools/session_guide.sh)
         if (const int64_t gd = opt(RT_OPT_GUIDE)) q.guide = (uint32_t)gd;  // diagnostics / A-B runs
         q.nslots = (uint32_t)nslots;
+        // the drain hand-over needs the streaming replay pass to resume the paths beside the fast
+        // kernel (the serialized pass would take them only after it): default 16 paths per wave
+        q.migrate = 0u;
+        if (!exact && !dev_ref.hrpp_tab && !(dp.tune & kModeReplayRef) && !(dp.tune & kModeNoStream)) {
+            const int64_t m = opt(RT_OPT_MIGRATE);
+            q.migrate = m < 0 ? kMigrateDefault : (uint32_t)m;
+        }
         if ((e = hipMemsetAsync(s->counter, 0, sizeof(TraceCounters), st)) != hipSuccess)
             return hip_fail(e, "memset counters");
         // the launch's camera behind the counters: the flat-list instances (kernel_flat.hip, RT_CAMMEM)
@@ -3791,6 +4178,7 @@ int rt_set_option(int option, int64_t value) {
         case RT_OPT_LAUNCH_LOG: ok = value == 0 || value == 1; break;
         case RT_OPT_BVH_BUILD: ok = value >= 0 && value <= 2; break;
         case RT_OPT_GUIDE: ok = value >= 0 && value <= 256; break;
+        case RT_OPT_MIGRATE: ok = value >= -1 && value <= 64; break;
     }
     if (!ok) return rthost::set_error(RT_ERR_INVALID, "option value out of range");
     g_opt[option].store(value, std::memory_order_relaxed);

@@ -25,7 +25,8 @@ from raytracinginoneweekendinrust_amd.configs import CONFIGS  # noqa: E402
 
 def bind(spec, idx):
     """spec: path.so, or path.so:0xTUNE (that library's RT_OPT_TUNE bits, e.g. 0x40 = the 3-wave
-    instance). Each spec loads its own copy of the file, so one build can be compared with itself."""
+    instance), or path.so:name=value,... (rt_set_option by tools/rtopts.py names, e.g.
+    migrate=0). Each spec loads its own copy of the file, so one build can be compared with itself."""
     import shutil
     import tempfile
     path, _, tune = spec.partition(":")
@@ -38,7 +39,10 @@ def bind(spec, idx):
     rtopts.apply_lib(lib)
     if tune:
         lib.rt_set_option.argtypes = [C.c_int, C.c_int64]
-        lib.rt_set_option(0, int(tune, 0))
+        for item in tune.split(","):
+            name, _, val = item.rpartition("=")
+            rc = lib.rt_set_option(rtopts.OPT_IDS[name] if name else 0, int(val, 0))
+            assert rc == 0, (spec, item, rc)
     lib.rt_scene_generate.argtypes = [C.c_char_p, C.c_uint64, C.c_char_p, C.POINTER(C.POINTER(_capi.rt_scene_desc))]
     lib.rt_scene_upload.argtypes = [C.POINTER(_capi.rt_scene_desc), C.c_int, C.POINTER(C.c_void_p)]
     lib.rt_render.argtypes = [C.c_void_p, C.POINTER(_capi.rt_camera_desc), C.POINTER(_capi.rt_render_params),
