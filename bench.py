@@ -176,6 +176,10 @@ def main() -> int:
     ap.add_argument("--exact-bvh", action="store_true")
     ap.add_argument("--gather", choices=["auto", "ipc", "shm"], default="auto",
                     help="N>1 frame gather transport (frame_gather.FrameGather)")
+    ap.add_argument("--pipeline", choices=["auto", "on", "off"], default="auto",
+                    help="two frames in flight per rank (two scene handles and streams): frame k+1's trace "
+                         "kernel takes the SIMDs frame k's last paths leave, and frame k is gathered while "
+                         "frame k+1 renders; auto = on for N>1 (strong scaling), off for one GPU")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -203,29 +207,56 @@ def main() -> int:
 
     cfg = rt.CONFIGS[args.config]
     scene = rt.Scene.generate(cfg.scene, cfg.scene_seed)
-    ds = rt.DeviceScene(scene, device=local_rank)
     cam = cfg.camera()
     W, H, spp = cfg.width, cfg.height, cfg.spp
     params, pixels_rank = rank_work(rt, cfg, rank, world, args.scaling, args.exact_bvh)
-    out = torch.zeros(W * H * 3, dtype=torch.float32, device="cuda")
-    seg = torch.zeros(1, dtype=torch.int64, device="cuda")
-    stream = torch.cuda.current_stream()
+    pipeline = args.pipeline == "on" or (args.pipeline == "auto" and world > 1)
+    nbuf = 2 if pipeline else 1
+    # one scene handle per frame in flight (each serialises its own launches and owns its sample buffer)
+    dss = [rt.DeviceScene(scene, device=local_rank) for _ in range(nbuf)]
+    outs = [torch.zeros(W * H * 3, dtype=torch.float32, device="cuda") for _ in range(nbuf)]
+    segs = [torch.zeros(1, dtype=torch.int64, device="cuda") for _ in range(nbuf)]
+    streams = [torch.cuda.Stream() for _ in range(nbuf)] if pipeline else [torch.cuda.current_stream()]
+    stream = streams[0]
     gather = None
     if args.scaling == "strong" and world > 1:
         from raytracinginoneweekendinrust_amd.frame_gather import FrameGather
         gather = FrameGather(W, H, rank, world, device=f"cuda:{local_rank}", transport=args.gather)
-    frame = [out]
+    frame = [outs[0]]
+    state = {"k": 0, "pending": None}
+
+    def finish(h):  # gather frame slot h (rank 0 ends holding the whole frame), ordered after its render
+        if gather is not None:
+            with torch.cuda.stream(streams[h]):
+                frame[0] = gather.gather(outs[h])
+        else:
+            frame[0] = outs[h]
 
     def step():
-        ds.launch(cam, params, out.data_ptr(), seg.data_ptr(), stream.cuda_stream)
-        if gather is not None:  # rank 0 ends the step holding the whole frame
-            frame[0] = gather.gather(out)
+        # render this step's frame; pipelined, the previous step's frame is gathered while it renders
+        h = state["k"] % nbuf
+        state["k"] += 1
+        dss[h].launch(cam, params, outs[h].data_ptr(), segs[h].data_ptr(), streams[h].cuda_stream)
+        if pipeline:
+            if state["pending"] is not None:
+                finish(state["pending"])
+            state["pending"] = h
+        else:
+            finish(h)
+
+    def flush():  # the last frame in flight
+        if state["pending"] is not None:
+            finish(state["pending"])
+            state["pending"] = None
 
     for _ in range(args.warmup):
         step()
+    flush()
     torch.cuda.synchronize()
-    ds.trace_time(reset=True)  # drop warmup launches from the per-launch timing
-    seg.zero_()
+    for d in dss:
+        d.trace_time(reset=True)  # drop warmup launches from the per-launch timing
+    for sg in segs:
+        sg.zero_()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -235,6 +266,10 @@ def main() -> int:
     ev0.record(stream)
     for _ in range(args.steps):
         step()
+    flush()
+    if pipeline:
+        for st_ in streams[1:]:
+            stream.wait_stream(st_)
     ev1.record(stream)
     torch.cuda.synchronize()
     if world > 1:
@@ -242,9 +277,13 @@ def main() -> int:
     t1 = time.perf_counter()
     wall = t1 - t0
     step_ms = ev0.elapsed_time(ev1) / args.steps          # device time of a whole step (all kernels)
-    trace_total_ms, trace_launches = ds.trace_time(reset=True)  # HIP events around each trace_samples launch
+    trace_total_ms, trace_launches = 0.0, 0
+    for d in dss:  # HIP events around each trace_samples launch
+        ms_, n_ = d.trace_time(reset=True)
+        trace_total_ms += ms_
+        trace_launches += n_
     kernel_ms = trace_total_ms / max(trace_launches, 1)
-    segments = int(seg.item())
+    segments = int(sum(int(sg.item()) for sg in segs))
     t = torch.tensor([wall, float(segments)], dtype=torch.float64)
     if world > 1:
         tw = t[:1].clone()
@@ -331,6 +370,9 @@ def main() -> int:
                                             "rt_shard_pull_unpack, or the /dev/shm bounce; no collective)" if world > 1
                                        else "one GPU: the whole frame"),
                        "gather": gather.transport if gather is not None else None,
+                       "pipeline": ("two frames in flight per rank: frame k+1 renders on a second scene handle and "
+                                    "stream while frame k drains and is gathered; every frame is complete and "
+                                    "gathered inside the timed region" if pipeline else None),
                        "exact_bvh": args.exact_bvh},
             "rays_per_s": seg_total / wall_max,
             "segments": int(seg_total),
@@ -358,7 +400,8 @@ def main() -> int:
         print(json.dumps(line), flush=True)
     if gather is not None:
         gather.close()
-    ds.close()
+    for d in dss:
+        d.close()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

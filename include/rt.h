@@ -309,10 +309,6 @@ int rt_bvh_build_order(const float* d_keys, uint32_t n, uint64_t seed, uint32_t*
  *                           (default), 1 = host always, 2 = device always
  *   RT_OPT_GUIDE            guided batch divisor K: a batch is at most (units left) /
  *                           (K x waves) units (1..256; 0 = the default 2)
- *   RT_OPT_MIGRATE          drain hand-over: once the work pool is dry, a fast-kernel wave with
- *                           at most this many paths left hands them to the streaming replay
- *                           pass, which resumes them packed into full waves (0..64; 0 = off;
- *                           -1 = the default 16)
  * Returns RT_ERR_INVALID for an unknown option or a value out of range. */
 typedef enum {
     RT_OPT_TUNE = 0,
@@ -323,8 +319,7 @@ typedef enum {
     RT_OPT_LAUNCH_LOG = 5,
     RT_OPT_BVH_BUILD = 6,
     RT_OPT_GUIDE = 7,
-    RT_OPT_MIGRATE = 8,
-    RT_OPT_COUNT = 9
+    RT_OPT_COUNT = 8
 } rt_option;
 int rt_set_option(int option, int64_t value);
 int rt_get_option(int option, int64_t* value);
@@ -427,7 +422,9 @@ int rt_device_numeric_eval(int op, const double* a, const double* b, double* out
  * four-child test — in: 14 floats per case (min[3], max[3], origin[3], direction[3],
  * t_min, t_max), out: (hit 1/0, entry t); op 2: Sphere::get_uv (sphere.rs:41-46) —
  * in: p[3], out: (u, v); op 3: Sphere::hit's root (sphere.rs:49-103) — in: center[3],
- * radius, origin[3], direction[3], t_min, t_max, out: (hit 1/0, t). */
+ * radius, origin[3], direction[3], t_min, t_max, out: (hit 1/0, t); op 4: the division
+ * from a correctly rounded reciprocal the kernel uses for a medium's cube sides — in: x, d,
+ * out: (div_rn(x, d, 1/d), x / d). */
 int rt_device_kat(int op, const float* in, float* out, uint32_t n);
 
 #ifdef __cplusplus

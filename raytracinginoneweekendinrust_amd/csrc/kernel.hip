@@ -542,6 +542,37 @@ RT_DEV bool msphere_t(f4 m0, f4 m1, f4 m2, const Ray& r, float tmin, float tmax,
     return true;
 }
 
+// Division from a correctly rounded reciprocal (Markstein): with inv = RN(1/d), q0 = RN(x * inv),
+// r = fma(-d, q0, x) (exact) and q = RN(q0 + r * inv) equals RN(x / d) whenever nothing under- or
+// overflows. Checked exhaustively over all 2^46 pairs of f32 significands (tools/markstein_check.hip,
+// profiles/r05/markstein_check.log: 0 mismatches); scaling x and d by powers of two scales every
+// step exactly, so the check covers every input the gate admits: |x| and |q0| in [2^-60, 2^60]
+// (then |d| and inv lie in [2^-121, 2^121] and r, r * inv are normal or r is 0). Anything else
+// (zeros, denormals, infinities, NaN, extreme ratios) takes the compiler's division.
+#ifndef RT_MARKSTEIN
+#define RT_MARKSTEIN 1
+#endif
+RT_DEV bool div_gate(float v) {  // |v| in [2^-60, 2^60], NaN excluded
+    return (__float_as_uint(v) & 0x7fffffffu) - 0x21800000u <= 0x5d800000u - 0x21800000u;
+}
+RT_DEV float div_rn(float x, float d, float inv) {
+    const float q0 = x * inv;
+    if (div_gate(x) && div_gate(q0)) return __builtin_fmaf(__builtin_fmaf(-d, q0, x), inv, q0);
+    return x / d;
+}
+// side_t with the direction component's reciprocal at hand (cube sides of a BVH leaf, a medium's
+// cube): the same quotient through div_rn.
+RT_DEV bool side_t_inv(float k, float ok, float dk, float dinv, float oa, float da, float ob, float db, float a0,
+                       float a1, float b0, float b1, float tmin, float tmax, float& t) {
+    const float tt = div_rn(k - ok, dk, dinv);
+    if (tt < tmin || tt > tmax) return false;
+    const float x = oa + tt * da;
+    const float y = ob + tt * db;
+    if (x < a0 || x > a1 || y < b0 || y > b1) return false;
+    t = tt;
+    return true;
+}
+
 // rectangle.rs:36-65 / 98-127 / 160-189; axis 0 = XY (plane z), 1 = XZ (plane y), 2 = YZ (plane x)
 // Selects between values, never between addresses (a select of struct-member
 // addresses pins the struct in scratch memory).
@@ -618,9 +649,9 @@ constexpr uint32_t kFSusp = 64u;
 [[maybe_unused]] constexpr uint32_t kStackLdsMax = 19u;  // LDS stack entries per lane at most (9.5 KB per wave: 16 waves/CU)
 // One leaf (primitive or cube). tmax = closest so far; a hit with t == closest is
 // accepted, so later candidates win ties exactly like hittable.rs:110-116.
-template <uint32_t kF = kFAll>
+template <uint32_t kF = kFAll, bool kInv = false>
 RT_DEV bool leaf_hit(const DevScene& S, uint32_t code, const Ray& r, const RayD& q, float tmin, float& closest,
-                     uint32_t& hit_code) {
+                     uint32_t& hit_code, V inv = V{0.0f, 0.0f, 0.0f}) {
     uint32_t type = rtdev::leaf_type(code), idx = rtdev::leaf_index(code);
     float t;
     if (type == rtdev::kLeafSphere) {
@@ -649,12 +680,41 @@ RT_DEV bool leaf_hit(const DevScene& S, uint32_t code, const Ray& r, const RayD&
         const float ox = r.o.x, oy = r.o.y, oz = r.o.z, dx = r.d.x, dy = r.d.y, dz = r.d.z;
         bool any = false;
         uint32_t face = 0u;
-        if (side_t(z0, oz, dz, ox, dx, oy, dy, x0, x1, y0, y1, tmin, closest, t)) { closest = t; face = 0u; any = true; }
-        if (side_t(z1, oz, dz, ox, dx, oy, dy, x0, x1, y0, y1, tmin, closest, t)) { closest = t; face = 1u; any = true; }
-        if (side_t(y0, oy, dy, ox, dx, oz, dz, x0, x1, z0, z1, tmin, closest, t)) { closest = t; face = 2u; any = true; }
-        if (side_t(y1, oy, dy, ox, dx, oz, dz, x0, x1, z0, z1, tmin, closest, t)) { closest = t; face = 3u; any = true; }
-        if (side_t(x0, ox, dx, oy, dy, oz, dz, y0, y1, z0, z1, tmin, closest, t)) { closest = t; face = 4u; any = true; }
-        if (side_t(x1, ox, dx, oy, dy, oz, dz, y0, y1, z0, z1, tmin, closest, t)) { closest = t; face = 5u; any = true; }
+        if constexpr (kInv && RT_MARKSTEIN) {  // the BVH traversal's reciprocals: no division per side
+            // the six quotients from the reciprocals (div_rn), one rare branch back to the divisions
+            float q[6] = {(z0 - oz) * inv.z, (z1 - oz) * inv.z, (y0 - oy) * inv.y,
+                          (y1 - oy) * inv.y, (x0 - ox) * inv.x, (x1 - ox) * inv.x};
+            const float num[6] = {z0 - oz, z1 - oz, y0 - oy, y1 - oy, x0 - ox, x1 - ox};
+            const float den[6] = {dz, dz, dy, dy, dx, dx}, rcp[6] = {inv.z, inv.z, inv.y, inv.y, inv.x, inv.x};
+            bool ok = true;
+#pragma unroll
+            for (int f = 0; f < 6; ++f) ok = ok && div_gate(num[f]) && div_gate(q[f]);
+            if (ok) {
+#pragma unroll
+                for (int f = 0; f < 6; ++f) q[f] = __builtin_fmaf(__builtin_fmaf(-den[f], q[f], num[f]), rcp[f], q[f]);
+            } else {
+#pragma unroll
+                for (int f = 0; f < 6; ++f) q[f] = num[f] / den[f];
+            }
+            auto side_q = [&](float tt, float oa, float da, float ob, float db, float a0, float a1, float b0, float b1) {
+                if (tt < tmin || tt > closest) return false;
+                const float x = oa + tt * da, y = ob + tt * db;
+                return !(x < a0 || x > a1 || y < b0 || y > b1);
+            };
+            if (side_q(q[0], ox, dx, oy, dy, x0, x1, y0, y1)) { closest = q[0]; face = 0u; any = true; }
+            if (side_q(q[1], ox, dx, oy, dy, x0, x1, y0, y1)) { closest = q[1]; face = 1u; any = true; }
+            if (side_q(q[2], ox, dx, oz, dz, x0, x1, z0, z1)) { closest = q[2]; face = 2u; any = true; }
+            if (side_q(q[3], ox, dx, oz, dz, x0, x1, z0, z1)) { closest = q[3]; face = 3u; any = true; }
+            if (side_q(q[4], oy, dy, oz, dz, y0, y1, z0, z1)) { closest = q[4]; face = 4u; any = true; }
+            if (side_q(q[5], oy, dy, oz, dz, y0, y1, z0, z1)) { closest = q[5]; face = 5u; any = true; }
+        } else {
+            if (side_t(z0, oz, dz, ox, dx, oy, dy, x0, x1, y0, y1, tmin, closest, t)) { closest = t; face = 0u; any = true; }
+            if (side_t(z1, oz, dz, ox, dx, oy, dy, x0, x1, y0, y1, tmin, closest, t)) { closest = t; face = 1u; any = true; }
+            if (side_t(y0, oy, dy, ox, dx, oz, dz, x0, x1, z0, z1, tmin, closest, t)) { closest = t; face = 2u; any = true; }
+            if (side_t(y1, oy, dy, ox, dx, oz, dz, x0, x1, z0, z1, tmin, closest, t)) { closest = t; face = 3u; any = true; }
+            if (side_t(x0, ox, dx, oy, dy, oz, dz, y0, y1, z0, z1, tmin, closest, t)) { closest = t; face = 4u; any = true; }
+            if (side_t(x1, ox, dx, oy, dy, oz, dz, y0, y1, z0, z1, tmin, closest, t)) { closest = t; face = 5u; any = true; }
+        }
         if (any) hit_code = rtdev::leaf_code(rtdev::kLeafRect, idx + face);
         return any;
     }
@@ -1162,236 +1222,9 @@ RT_DEV bool bvh_hit(const DevScene& S, float delta, uint32_t root, const Ray& r,
 // false; the walk resumes it on a later trip of the sample loop, together with the lanes
 // that reach the same BVH then. The visit order and every value are unchanged, only when a
 // visit runs differs, so the result is the same bits.
-#ifndef RT_EXP_TRIP
-#define RT_EXP_TRIP 1
-#endif
-// The fast BVH4 traversal without leaf postponement (every preset but the triangle one, and the
-// replay pass): one node per trip; a leaf node's 1-2 leaves are tested at once, an interior
-// node's four slots get the packed box test, the sort network and the pushes only on the
-// interior branch (a leaf trip goes straight to the pop), and a pop reads an entry's node and
-// key together. Same visits, same candidates, same merge as bvh_run's general loop.
-template <int kKind, uint32_t kF>
-RT_DEV void bvh_run_immediate(const DevScene& S, float delta, const f4* wrapper, const Ray& r, V inv, float tmin,
-                              float& closest, uint32_t& hit_code, uint32_t* stk, uint32_t mode, Trav& tv) {
-    const float tmax_entry = tv.tmax_entry;
-    const bool prune = (__float_as_uint(wrapper[7].w) & rtdev::kBvhPrunable) != 0u || (mode & kModePruneAllExp);
-    const float dmi = delta * fmaxf(fmaxf(__builtin_fabsf(inv.x), __builtin_fabsf(inv.y)), __builtin_fabsf(inv.z));
-    const bool leaf_boxes = prune && !(mode & kModeNoLeafBoxes);
-    [[maybe_unused]] const uint32_t hnx = inv.x < 0.0f ? 48u : 0u, hny = inv.y < 0.0f ? 64u : 16u,
-                                    hnz = inv.z < 0.0f ? 80u : 32u;
-    bool any = tv.any;
-    uint32_t best_rank = tv.best_rank, sp = tv.sp, cur = tv.cur;
-#ifdef RT_PROFILE_REGIONS
-    uint32_t visits = 0;
-#endif
-    for (;;) {
-        uint32_t onx, ony, onz;  // near-plane row offsets (bvh_run)
-        if constexpr ((kF & kFTri) != 0u) {
-            onx = hnx;
-            ony = hny;
-            onz = hnz;
-        } else {
-            uint32_t msx, msy, msz;
-            asm volatile("v_ashrrev_i32 %0, 31, %1" : "=v"(msx) : "v"(inv.x));
-            asm volatile("v_ashrrev_i32 %0, 31, %1" : "=v"(msy) : "v"(inv.y));
-            asm volatile("v_ashrrev_i32 %0, 31, %1" : "=v"(msz) : "v"(inv.z));
-            onx = msx & 48u;
-            ony = (msy & 48u) + 16u;
-            onz = (msz & 48u) + 32u;
-        }
-#ifdef RT_LEAF_AUDIT
-        if ((cur & ~rtdev::kLeafNodeFlag) >= S.num_nodes || sp > S.stack_depth + S.spill_depth) {
-            atomicAdd(&g_bounds_audit_count, 1u);
-            break;
-        }
-#endif
-#ifdef RT_PROFILE_REGIONS
-        ++visits;
-#endif
-        PROF_T0(pt);
-        if ((cur & rtdev::kLeafNodeFlag) != 0u) {
-            // the 1-2 leaves of one reference BVH2 node, formed like bvh.rs:377-414 (bvh_run)
-            const uint32_t nbo = (cur & ~rtdev::kLeafNodeFlag) * (rtdev::kBvhNodeF4 * 16u);
-            const f4* nd = S.nodes;
-            const float2 nx2 = ld2_at(nd, nbo + onx), ny2 = ld2_at(nd, nbo + ony), nz2 = ld2_at(nd, nbo + onz),
-                         fx2 = ld2_at(nd, nbo + (onx ^ 48u)), fy2 = ld2_at(nd, nbo + (ony ^ 80u)),
-                         fz2 = ld2_at(nd, nbo + (onz ^ 112u)), chs = ld2_at(nd, nbo + 96u), rks = ld2_at(nd, nbo + 112u);
-            float tmr = tmax_entry, nt = 0.0f;
-            bool nh = false;
-            uint32_t ncode = 0u, nrank = 0u;
-            const uint32_t nleaf = __float_as_uint(chs.y) == rtdev::kChildEmpty ? 1u : 2u;
-            float llo[2] = {-kInf, -kInf}, lhi[2] = {kInf, kInf};
-            if (leaf_boxes) leaf_intervals2_nf(nx2, ny2, nz2, fx2, fy2, fz2, r, inv, delta, llo, lhi);
-            for (uint32_t k = 0; k < nleaf; ++k) {
-                const uint32_t lcode = __float_as_uint(k ? chs.y : chs.x), rank = __float_as_uint(k ? rks.y : rks.x);
-#ifdef RT_LEAF_AUDIT
-                const float2 bx0 = ld2(S.nodes + nbo / 16u, 0), by0 = ld2(S.nodes + nbo / 16u, 1),
-                             bz0 = ld2(S.nodes + nbo / 16u, 2), bx1 = ld2(S.nodes + nbo / 16u, 3),
-                             by1 = ld2(S.nodes + nbo / 16u, 4), bz1 = ld2(S.nodes + nbo / 16u, 5);
-                const float x0 = k ? bx0.y : bx0.x, y0 = k ? by0.y : by0.x, z0 = k ? bz0.y : bz0.x;
-                const float x1 = k ? bx1.y : bx1.x, y1 = k ? by1.y : by1.x, z1 = k ? bz1.y : bz1.x;
-#endif
-                const float bound = tmr < closest ? tmr : closest;
-                if (!leaf_boxes || leaf_interval_may_hit(k ? llo[1] : llo[0], k ? lhi[1] : lhi[0], tmin, bound)) {
-                    PROF_T0(pl);
-                    const float cap = closest < kInf ? __uint_as_float(__float_as_uint(closest) + 1u) : kInf;
-                    float c = tmr < cap ? tmr : cap;
-                    uint32_t code = 0u;
-                    const RayD q = to_d(r);
-                    if (leaf_hit<kF>(S, lcode, r, q, tmin, c, code)) {
-                        const uint32_t rk = rank + (rtdev::leaf_type(lcode) == rtdev::kLeafCube
-                                                        ? rtdev::leaf_index(code) - rtdev::leaf_index(lcode)
-                                                        : 0u);
-                        if (!nh || !(nt < c)) {
-                            nh = true;
-                            nt = c;
-                            ncode = code;
-                            nrank = rk;
-                        }
-                        tmr = c;
-                    }
-                    PROF_ADD(kPrLeafTest, pl);
-                } else {
-                    LEAF_AUDIT(lcode, rank, x0, y0, z0, x1, y1, z1);
-                }
-            }
-            if (nh && (nt < closest || (nt == closest && nrank > best_rank))) {
-                closest = nt;
-                best_rank = nrank;
-                hit_code = ncode;
-                any = true;
-            }
-            PROF_ADD(kPrBvhTrip, pt);
-        } else {
-            const uint32_t nbo = cur * (rtdev::kBvhNodeF4 * 16u);
-            const f4* nd = S.nodes;
-            const f4 nx = ld4_at(nd, nbo + onx), ny = ld4_at(nd, nbo + ony), nz = ld4_at(nd, nbo + onz),
-                     fx = ld4_at(nd, nbo + (onx ^ 48u)), fy = ld4_at(nd, nbo + (ony ^ 80u)),
-                     fz = ld4_at(nd, nbo + (onz ^ 112u)), chf = ld4_at(nd, nbo + 96u);
-            uint32_t c0 = __float_as_uint(chf.x), c1 = __float_as_uint(chf.y), c2 = __float_as_uint(chf.z),
-                     c3 = __float_as_uint(chf.w);
-            float key[4];
-            child_keys4_nf(nx, ny, nz, fx, fy, fz, r, inv, tmin, tmax_entry, prune ? prune_bound(closest) : kInf,
-                           prune ? dmi : 0.0f, key);
-            float t0 = key[0], t1 = key[1], t2 = key[2], t3 = key[3];
-            PROF_ADD(kPrBvhTrip, pt);
-            PROF_T0(pp);
-#if defined(RT_EXP_NOSORT) && RT_EXP_NOSORT
-            // EXPERIMENT (A/B only): no sort network. Slots in DFS order (1), or reversed when the
-            // ray runs against the node's top split axis (2, the axis in the rank row's low bits);
-            // the first passing slot is visited next and the others pushed in reverse, so the
-            // order approximates near-first. Same visit set, same merge: the same bits.
-            if (RT_EXP_NOSORT == 2) {
-                const uint32_t ax = __float_as_uint(ld2_at(nd, nbo + 112u).x) & 3u;
-                const float dax = ax == 0u ? r.d.x : (ax == 1u ? r.d.y : r.d.z);
-                if (dax < 0.0f) {
-                    float tt = t0; t0 = t3; t3 = tt; tt = t1; t1 = t2; t2 = tt;
-                    uint32_t cc = c0; c0 = c3; c3 = cc; cc = c1; c1 = c2; c2 = cc;
-                }
-            }
-            {
-                const bool v0 = t0 != kInf, v1 = t1 != kInf, v2 = t2 != kInf, v3 = t3 != kInf;
-                if (v0 || v1 || v2 || v3) {
-                    auto push = [&](uint32_t node, float t) {
-                        if (!(kF & kFDeep) || sp < S.stack_depth) {
-                            stk[sp * 128u] = node;
-                            stk[sp * 128u + 64u] = __float_as_uint(t);
-                        } else {
-                            uint32_t* g = S.stack_spill +
-                                          (((size_t)blockIdx.x * S.spill_depth + (sp - S.stack_depth)) * 64u + threadIdx.x) * 2u;
-                            g[0] = node;
-                            g[1] = __float_as_uint(t);
-                        }
-                        sp += 1u;
-                    };
-                    if (v3 && (v0 || v1 || v2)) push(c3, t3);
-                    if (v2 && (v0 || v1)) push(c2, t2);
-                    if (v1 && v0) push(c1, t1);
-                    cur = v0 ? c0 : (v1 ? c1 : (v2 ? c2 : c3));
-                    PROF_ADD(kPrBvhPush, pp);
-                    continue;
-                }
-            }
-#else
-            sort2(t0, c0, t1, c1);
-            sort2(t2, c2, t3, c3);
-            sort2(t0, c0, t2, c2);
-            sort2(t1, c1, t3, c3);
-            sort2(t1, c1, t2, c2);
-#endif
-            if (t0 != kInf) {  // visit the nearest next, push the others far to near
-                auto push = [&](uint32_t node, float t) {
-                    if (!(kF & kFDeep) || sp < S.stack_depth) {
-                        stk[sp * 128u] = node;
-                        stk[sp * 128u + 64u] = __float_as_uint(t);
-                    } else {
-                        uint32_t* g = S.stack_spill +
-                                      (((size_t)blockIdx.x * S.spill_depth + (sp - S.stack_depth)) * 64u + threadIdx.x) * 2u;
-                        g[0] = node;
-                        g[1] = __float_as_uint(t);
-                    }
-                    sp += 1u;
-                };
-                if (t3 != kInf) push(c3, t3);
-                if (t2 != kInf) push(c2, t2);
-                if (t1 != kInf) push(c1, t1);
-                cur = c0;
-                PROF_ADD(kPrBvhPush, pp);
-                continue;
-            }
-            PROF_ADD(kPrBvhPush, pp);
-        }
-        PROF_T0(ppop);
-        // pop the nearest-pushed entry whose key the current bound does not prune
-        const float pb = prune ? prune_bound(closest) : kInf;
-        bool found = false;
-        while (sp > 0u) {
-            sp -= 1u;
-            uint32_t cand, tb;
-            if (!(kF & kFDeep) || sp < S.stack_depth) {
-                cand = stk[sp * 128u];
-                tb = stk[sp * 128u + 64u];
-            } else {
-                const uint32_t* g = S.stack_spill +
-                                    (((size_t)blockIdx.x * S.spill_depth + (sp - S.stack_depth)) * 64u + threadIdx.x) * 2u;
-                cand = g[0];
-                tb = g[1];
-            }
-            if (!(__uint_as_float(tb) > pb)) {
-                cur = cand;
-                found = true;
-                break;
-            }
-        }
-        PROF_ADD(kPrBvhPop, ppop);
-        if (!found) break;
-    }
-    tv = Trav{cur, sp, best_rank, tmax_entry, any, kNoNode};
-#ifdef RT_PROFILE_REGIONS
-    {
-        const uint32_t b = trips_bin(visits);
-        uint32_t m = visits;
-        for (int off = 32; off > 0; off >>= 1) {
-            uint32_t o = __shfl_xor(m, off);
-            m = o > m ? o : m;
-        }
-        const uint32_t first = (uint32_t)__builtin_ctzll(__ballot(1));
-        for (uint32_t bin = 0; bin < 8u; ++bin) {
-            const uint32_t n = (uint32_t)__popcll(__ballot(b == bin));
-            if (__lane_id() == first && n) prof_lds[3u * kPrCount + bin] += n;
-        }
-        if (__lane_id() == first) prof_lds[3u * kPrCount + 8u + trips_bin(m)] += 1u;
-    }
-#endif
-}
-
 template <int kKind, uint32_t kF, bool kSusp>
 RT_DEV bool bvh_run(const DevScene& S, float delta, const f4* wrapper, const Ray& r, V inv, float tmin, float& closest,
                     uint32_t& hit_code, uint32_t* stk, uint32_t mode, Trav& tv, uint32_t susp) {
-    if constexpr (RT_EXP_TRIP && !kSusp && !((kF & kFTri) != 0u && kKind == 0)) {
-        bvh_run_immediate<kKind, kF>(S, delta, wrapper, r, inv, tmin, closest, hit_code, stk, mode, tv);
-        return true;
-    }
     const float tmax_entry = tv.tmax_entry;
     const bool prune = (__float_as_uint(wrapper[7].w) & rtdev::kBvhPrunable) != 0u || (mode & kModePruneAllExp);
     const float dmi = delta * fmaxf(fmaxf(__builtin_fabsf(inv.x), __builtin_fabsf(inv.y)), __builtin_fabsf(inv.z));
@@ -1716,6 +1549,30 @@ RT_DEV void spheres_surely_missed2(f4 s0, f4 s1, const Ray& r, float a, bool& m0
 #ifndef RT_EXP_UNIFORM_RECT
 #define RT_EXP_UNIFORM_RECT 1
 #endif
+#ifndef RT_EXP_UNIFORM_ENTRY
+#define RT_EXP_UNIFORM_ENTRY 1
+#endif
+// A top-level entry's record is the same for every lane of the wave (the list walk is a
+// wave-uniform loop): its fields are read once into scalar registers (readfirstlane), so the
+// wave branches on them instead of masking lanes.
+RT_DEV uint32_t uni(uint32_t v) {
+#if RT_EXP_UNIFORM_ENTRY
+    return __builtin_amdgcn_readfirstlane(v);
+#else
+    return v;
+#endif
+}
+// apply_op for a wave-uniform transform record: the Translate / RotateY choice is a scalar branch.
+RT_DEV Ray apply_op_u(f4 op, Ray r) {
+    if (__uint_as_float(uni(__float_as_uint(op.w))) == 0.0f) {
+        r.o = r.o - xyz(op);
+    } else {
+        float s = op.x, c = op.y;
+        r.o = mk(c * r.o.x - s * r.o.z, r.o.y, s * r.o.x + c * r.o.z);
+        r.d = mk(c * r.d.x - s * r.d.z, r.d.y, s * r.d.x + c * r.d.z);
+    }
+    return r;
+}
 constexpr uint32_t kRunPretestMin = 8u;  // sphere runs at least this long take the f32 pretest
 // A GEOM or BVH entry (the caller guarantees E is wave-uniform). Only instances
 // with kFRuns carry the f32 pretest of long sphere runs, only those with kFBvh the
@@ -1723,10 +1580,11 @@ constexpr uint32_t kRunPretestMin = 8u;  // sphere runs at least this long take 
 template <int kKind, uint32_t kF>
 RT_DEV bool entry_geom_hit(const DevScene& S, float delta, const DevEntry* E, Ray r, float tmin, float& closest,
                            uint32_t& hit_code, uint32_t* stk, uint32_t mode, bool& replay) {
-    uint32_t ntf = E->ntf;
-    for (uint32_t i = 0; i < ntf; ++i) r = apply_op(E->tf[i], r);
-    if (E->kind == rtdev::kEntSphereRun) {  // consecutive top-level spheres, in list order
-        const uint32_t first = E->payload, n = E->pad[0];
+    uint32_t ntf = uni(E->ntf);
+    for (uint32_t i = 0; i < ntf; ++i) r = apply_op_u(E->tf[i], r);
+    const uint32_t kind = uni(E->kind);
+    if (kind == rtdev::kEntSphereRun) {  // consecutive top-level spheres, in list order
+        const uint32_t first = uni(E->payload), n = uni(E->pad[0]);
         const RayD q = to_d(r);
         const bool pretest = (kF & kFRuns) && n >= kRunPretestMin && !(mode & kModeNoPretest);  // long lists (random_spheres without a BVH): most spheres are misses
         bool any = false;
@@ -1761,14 +1619,14 @@ RT_DEV bool entry_geom_hit(const DevScene& S, float delta, const DevEntry* E, Ra
         }
         return any;
     }
-    if (E->kind == rtdev::kEntBvh) {
+    if (kind == rtdev::kEntBvh) {
         if constexpr ((kF & kFBvh) == 0u) {
             return false;  // not reached: the scene has no BVH
         } else {
             ABLATE(kAbBvh2, float c2 = closest; uint32_t h2 = 0u; bool rp = false;
                    if (bvh_hit<kKind, kF>(S, delta, E->payload, r, tmin, c2, h2, stk, mode, rp) && h2 == 0x7fffffffu)
                        closest = -1.0f;);
-            return bvh_hit<kKind, kF>(S, delta, E->payload, r, tmin, closest, hit_code, stk, mode, replay);
+            return bvh_hit<kKind, kF>(S, delta, uni(E->payload), r, tmin, closest, hit_code, stk, mode, replay);
         }
     }
 #if RT_EXP_UNIFORM_RECT
@@ -1800,7 +1658,7 @@ RT_DEV bool entry_geom_hit(const DevScene& S, float delta, const DevEntry* E, Ra
     RayD q = to_d(r);
     ABLATE(kAbGeom2, float c2 = closest; uint32_t h2 = 0u;
            if (leaf_hit<kF | kFLeafRM>(S, E->payload, r, q, tmin, c2, h2) && h2 == 0x7fffffffu) closest = -1.0f;);
-    return leaf_hit<kF | kFLeafRM>(S, E->payload, r, q, tmin, closest, hit_code);  // top level: any primitive
+    return leaf_hit<kF | kFLeafRM>(S, uni(E->payload), r, q, tmin, closest, hit_code);  // top level: any primitive
 }
 
 // ConstantMedium::hit (hittable.rs:176-233); draws one U(0,1) once the clamped
@@ -1808,23 +1666,23 @@ RT_DEV bool entry_geom_hit(const DevScene& S, float delta, const DevEntry* E, Ra
 template <int kKind, uint32_t kF>
 RT_DEV bool medium_hit(const DevScene& S, float delta, const DevEntry* E, Ray r, float tmin, float tmax, Rng& g,
                        const Key& k, float& t_out, uint32_t* stk, uint32_t mode, bool& replay) {
-    uint32_t ntf = E->ntf;
-    for (uint32_t i = 0; i < ntf; ++i) r = apply_op(E->tf[i], r);
-    const DevEntry* B = S.entries + E->payload;
+    uint32_t ntf = uni(E->ntf);
+    for (uint32_t i = 0; i < ntf; ++i) r = apply_op_u(E->tf[i], r);
+    const DevEntry* B = S.entries + uni(E->payload);
     float t1 = kInf, t2 = kInf;
-    if (B->kind == rtdev::kEntGeom && rtdev::leaf_type(B->payload) == rtdev::kLeafSphere) {
+    const uint32_t bkind = uni(B->kind), bcode = uni(B->payload);
+    if (bkind == rtdev::kEntGeom && rtdev::leaf_type(bcode) == rtdev::kLeafSphere) {
         // boundary.hit(-inf, inf) then boundary.hit(t1 + 1e-4, inf) on one sphere:
         // the same two roots, selected against two intervals.
         Ray rb = r;
-        uint32_t bn = B->ntf;
-        for (uint32_t i = 0; i < bn; ++i) rb = apply_op(B->tf[i], rb);
-        Roots R = sphere_roots(ld4(S.sph + rtdev::leaf_index(B->payload)), to_d(rb));
+        uint32_t bn = uni(B->ntf);
+        for (uint32_t i = 0; i < bn; ++i) rb = apply_op_u(B->tf[i], rb);
+        Roots R = sphere_roots(ld4(S.sph + rtdev::leaf_index(bcode)), to_d(rb));
         ABLATE(kAbMedium2, Roots R2 = sphere_roots(ld4(S.sph + rtdev::leaf_index(B->payload)), to_d(rb));
                if (R2.r1 == -1.0) t1 = -1.0f;);
         if (!sphere_select(R, -kInf, kInf, t1)) return false;
         if (!sphere_select(R, t1 + 0.0001f, kInf, t2)) return false;
-    } else if ((kF & kFTri) == 0u && B->kind == rtdev::kEntGeom &&
-               rtdev::leaf_type(B->payload) == rtdev::kLeafCube) {
+    } else if ((kF & kFTri) == 0u && bkind == rtdev::kEntGeom && rtdev::leaf_type(bcode) == rtdev::kLeafCube) {
         // boundary.hit twice on one Cube (cube.rs:84-93, six sides in list order): each
         // side's t = (k - o) / d and its in-rectangle test do not depend on the interval,
         // so they are computed once and both calls replay the list's selection on them,
@@ -1832,28 +1690,53 @@ RT_DEV bool medium_hit(const DevScene& S, float delta, const DevEntry* E, Ray r,
         // same bits). Left out of the triangle preset, whose scenes have no cube media and
         // whose register allocation the unused code cost 2.7% (C4).
         Ray rb = r;
-        uint32_t bn = B->ntf;
-        for (uint32_t i = 0; i < bn; ++i) rb = apply_op(B->tf[i], rb);
-        const uint32_t idx = rtdev::leaf_index(B->payload);
+        uint32_t bn = uni(B->ntf);
+        for (uint32_t i = 0; i < bn; ++i) rb = apply_op_u(B->tf[i], rb);
+        const uint32_t idx = rtdev::leaf_index(bcode);
         const f4 s0 = ld4(S.rect + 2 * idx);
         const float y1 = ld2(S.rect + 2 * idx + 1, 0).x, z1 = ld2(S.rect + 2 * idx + 5, 0).x;
         const float x0 = s0.y, x1 = s0.z, y0 = s0.w, z0 = s0.x;
         const float ox = rb.o.x, oy = rb.o.y, oz = rb.o.z, dx = rb.d.x, dy = rb.d.y, dz = rb.d.z;
         float tt[6];
         uint32_t in = 0u;  // bit f: side f's point lies inside its rectangle (rectangle.rs:36-65)
-        auto side = [&](int f, float k, float ok, float dk, float oa, float da, float ob, float db, float a0, float a1,
-                        float b0, float b1) {
-            const float t = (k - ok) / dk;
-            const float x = oa + t * da, y = ob + t * db;
-            tt[f] = t;
+        {
+            const float num[6] = {z0 - oz, z1 - oz, y0 - oy, y1 - oy, x0 - ox, x1 - ox};
+            const float den[6] = {dz, dz, dy, dy, dx, dx};
+            if constexpr (RT_MARKSTEIN && (kF & (kFBvh | kFRuns)) == 0u) {
+            // three reciprocals (the reference divides by each direction component twice), the six
+            // quotients from them (div_rn), one rare branch back to the divisions; the flat-list
+            // preset only (C5's smoke boxes): in the others the extra live values cost spilled
+            // registers (C3's instance 20 -> 32 VGPRs, C2's 19 -> 25) for code they rarely run
+            const float ix = 1.0f / dx, iy = 1.0f / dy, iz = 1.0f / dz;
+            const float rcp[6] = {iz, iz, iy, iy, ix, ix};
+            bool ok = true;
+#pragma unroll
+            for (int f = 0; f < 6; ++f) {
+                tt[f] = num[f] * rcp[f];
+                ok = ok && div_gate(num[f]) && div_gate(tt[f]);
+            }
+            if (ok) {
+#pragma unroll
+                for (int f = 0; f < 6; ++f) tt[f] = __builtin_fmaf(__builtin_fmaf(-den[f], tt[f], num[f]), rcp[f], tt[f]);
+            } else {
+#pragma unroll
+                for (int f = 0; f < 6; ++f) tt[f] = num[f] / den[f];
+            }
+            } else {
+#pragma unroll
+                for (int f = 0; f < 6; ++f) tt[f] = num[f] / den[f];
+            }
+        }
+        auto side = [&](int f, float oa, float da, float ob, float db, float a0, float a1, float b0, float b1) {
+            const float x = oa + tt[f] * da, y = ob + tt[f] * db;
             if (!(x < a0 || x > a1 || y < b0 || y > b1)) in |= 1u << f;
         };
-        side(0, z0, oz, dz, ox, dx, oy, dy, x0, x1, y0, y1);
-        side(1, z1, oz, dz, ox, dx, oy, dy, x0, x1, y0, y1);
-        side(2, y0, oy, dy, ox, dx, oz, dz, x0, x1, z0, z1);
-        side(3, y1, oy, dy, ox, dx, oz, dz, x0, x1, z0, z1);
-        side(4, x0, ox, dx, oy, dy, oz, dz, y0, y1, z0, z1);
-        side(5, x1, ox, dx, oy, dy, oz, dz, y0, y1, z0, z1);
+        side(0, ox, dx, oy, dy, x0, x1, y0, y1);
+        side(1, ox, dx, oy, dy, x0, x1, y0, y1);
+        side(2, ox, dx, oz, dz, x0, x1, z0, z1);
+        side(3, ox, dx, oz, dz, x0, x1, z0, z1);
+        side(4, oy, dy, oz, dz, y0, y1, z0, z1);
+        side(5, oy, dy, oz, dz, y0, y1, z0, z1);
         auto pick = [&](float lo, float& closest) {  // the HittableList walk: closest narrows
             bool any = false;
 #pragma unroll
@@ -2308,7 +2191,6 @@ struct ChunkParams {
     uint32_t nslots;          // sample-buffer plane size: 64 slots per 8x8 block of the shard, block-major
     uint32_t group;           // units per batch at most (batch_group)
     uint32_t blocks;          // 8x8 blocks of the shard (units = blocks x samples)
-    uint32_t migrate;         // drain hand-over: a dry wave with at most this many paths left hands them over (0: off)
 };
 
 // HittableList::hit over the world (hittable.rs:100-118), t in [0.001, inf).
@@ -2320,7 +2202,7 @@ RT_DEV bool world_hit(const DevScene& S, float delta, const Ray& r, Rng& g, cons
     for (uint32_t e = 0; e < S.num_top; ++e) {
         const DevEntry* E = S.entries + e;
         PROF_T0(pe);
-        if (E->kind == rtdev::kEntMedium) {
+        if (uni(E->kind) == rtdev::kEntMedium) {
             float t;
             if (medium_hit<kKind, kF>(S, delta, E, r, 0.001f, closest, g, k, t, stk, mode, replay)) {
                 closest = t;
@@ -2365,7 +2247,8 @@ RT_DEV void world_walk(const DevScene& S, float delta, const Ray& ray, Rng& g, c
         if (!(active && w.pos == e)) continue;
         PROF_T0(pe);
         const DevEntry* E = S.entries + e;
-        if (E->kind == rtdev::kEntMedium) {
+        const uint32_t kind = uni(E->kind);
+        if (kind == rtdev::kEntMedium) {
             float t;
             if (medium_hit<0, kF>(S, delta, E, ray, 0.001f, w.closest, g, k, t, stk, mode, replay)) {
                 w.closest = t;
@@ -2374,11 +2257,11 @@ RT_DEV void world_walk(const DevScene& S, float delta, const Ray& ray, Rng& g, c
                 w.any = true;
             }
             w.pos = e + 1u;
-        } else if ((kF & kFBvh) && E->kind == rtdev::kEntBvh) {
+        } else if ((kF & kFBvh) && kind == rtdev::kEntBvh) {
             Ray r = ray;
-            const uint32_t ntf = E->ntf;
-            for (uint32_t i = 0; i < ntf; ++i) r = apply_op(E->tf[i], r);
-            const uint32_t root = E->payload;
+            const uint32_t ntf = uni(E->ntf);
+            for (uint32_t i = 0; i < ntf; ++i) r = apply_op_u(E->tf[i], r);
+            const uint32_t root = uni(E->payload);
             const f4* wrapper = S.nodes + (size_t)root * rtdev::kBvhNodeF4;
             const V inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
             if (!w.resume) {  // bvh_hit's hand-over rule (NaN-prone rays go to the reference kernel)
@@ -2437,7 +2320,6 @@ struct TraceCounters {
     unsigned fast_done;          // fast-kernel waves that have finished (the streaming replay's end)
     unsigned stream_abort;       // the streaming replay gave up a claimed entry: re-render the chunk
     unsigned long long fast_segments;  // segments of the fast kernel's and streaming replay's samples
-    unsigned migrate_count;      // path records the fast kernel's draining waves handed over (below)
 };
 // A replay-list entry: the sample's pixel and its chunk-local sample index. Entries are
 // written and read as one 64-bit agent-scope atomic: the streaming replay pass reads them
@@ -2464,44 +2346,6 @@ RT_DEV ReplayItem replay_take(const ReplayItem* list, uint32_t idx) {
     return ReplayItem{(uint32_t)v, (uint32_t)(v >> 32)};
 }
 constexpr uint32_t kReplayCap = 1u << 20;
-// The drain hand-over. Once the work pool is dry, a fast-kernel wave with at most Q.migrate
-// paths still running writes each path's whole state (PathRecord) behind the replay list and
-// publishes it as a replay entry flagged kMigrated, then exits. The streaming replay pass, which
-// takes the slots the fast kernel's waves leave, resumes those paths where they stopped, packed
-// into full waves: the last long paths of a launch run in few waves instead of one or two lanes
-// of many waves that share every SIMD's issue slots. A path continues from the same state with
-// the same Philox stream, so its result and segment count are the ones it would have had.
-constexpr uint32_t kMigrateCap = 1u << 16;
-constexpr uint32_t kMigrated = 0x80000000u;  // ReplayItem.sample flag: .pixel is a path record index
-#ifndef RT_MIGRATE_DEFAULT
-#define RT_MIGRATE_DEFAULT 16
-#endif
-constexpr uint32_t kMigrateDefault = RT_MIGRATE_DEFAULT;  // rt_set_option(RT_OPT_MIGRATE, -1)
-constexpr uint32_t kPathRecordU4 = 6u;  // a path record: 6 x 16 B behind the replay list
-RT_DEV uint4* path_records(const ReplayItem* list) {
-    return reinterpret_cast<uint4*>(const_cast<ReplayItem*>(list) + kReplayCap);
-}
-RT_DEV void save_path(uint4* rec, uint32_t slot, uint32_t s_local, uint32_t depth, const Rng& g, V L, V T,
-                      const Ray& ray) {
-    rec[0] = make_uint4(slot, s_local, depth, g.sample);
-    rec[1] = make_uint4(g.pixel, g.d, g.r0, g.r1);
-    rec[2] = make_uint4(g.r2, __float_as_uint(L.x), __float_as_uint(L.y), __float_as_uint(L.z));
-    rec[3] = make_uint4(__float_as_uint(T.x), __float_as_uint(T.y), __float_as_uint(T.z), __float_as_uint(ray.time));
-    rec[4] = make_uint4(__float_as_uint(ray.o.x), __float_as_uint(ray.o.y), __float_as_uint(ray.o.z),
-                        __float_as_uint(ray.d.x));
-    rec[5] = make_uint4(__float_as_uint(ray.d.y), __float_as_uint(ray.d.z), 0u, 0u);
-}
-RT_DEV void load_path(const uint4* rec, uint32_t& slot, uint32_t& s_local, uint32_t& depth, Rng& g, V& L, V& T,
-                      Ray& ray) {
-    const uint4 a = rec[0], b = rec[1], c = rec[2], d = rec[3], e = rec[4], f = rec[5];
-    slot = a.x; s_local = a.y; depth = a.z; g.sample = a.w;
-    g.pixel = b.x; g.d = b.y; g.r0 = b.z; g.r1 = b.w;
-    g.r2 = c.x; L = mk(__uint_as_float(c.y), __uint_as_float(c.z), __uint_as_float(c.w));
-    T = mk(__uint_as_float(d.x), __uint_as_float(d.y), __uint_as_float(d.z));
-    ray.time = __uint_as_float(d.w);
-    ray.o = mk(__uint_as_float(e.x), __uint_as_float(e.y), __uint_as_float(e.z));
-    ray.d = mk(__uint_as_float(e.w), __uint_as_float(f.x), __uint_as_float(f.y));
-}
 // The streaming replay pass (trace_samples<3> with fixup 2, on a second stream) claims
 // entries one at a time while the fast kernel drains. Returns the claimed entry's index once
 // it is published, or kReplayNone when the fast kernel finished without one, the list
@@ -2509,34 +2353,6 @@ RT_DEV void load_path(const uint4* rec, uint32_t& slot, uint32_t& s_local, uint3
 constexpr uint32_t kReplayNone = 0xffffffffu;
 constexpr uint32_t kStreamWaves = 512;  // waves of the streaming replay pass
 constexpr unsigned long long kStreamTimeoutTicks = 1000000000ull;  // 10 s of s_memrealtime (100 MHz)
-// With the drain hand-over on (Q.migrate), one claim takes `cnt` consecutive entries and waits until
-// every one of them is published, or until the fast kernel has finished without producing the
-// last ones (cnt then shrinks to the entries that exist: none is lost, the count is final).
-RT_DEV uint32_t replay_claim_n(TraceCounters* ctr, const ReplayItem* list, uint32_t fast_grid, uint32_t& cnt) {
-    const uint32_t i = atomicAdd(&ctr->replay_pull, cnt);
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    for (;;) {
-        const bool done = __hip_atomic_load(&ctr->fast_done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) >= fast_grid;
-        const uint32_t n = __hip_atomic_load(&ctr->replay_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (i >= kReplayCap) return kReplayNone;
-        if (done || n >= i + cnt) {
-            uint32_t e = i + cnt < n ? i + cnt : n;
-            e = e < kReplayCap ? e : kReplayCap;
-            if (e <= i) return kReplayNone;
-            uint32_t j = i;
-            while (j < e && replay_peek(list, j) != kReplayFree) ++j;
-            if (j == e) {
-                cnt = e - i;
-                return i;
-            }
-        }
-        if (__builtin_amdgcn_s_memrealtime() - t0 > kStreamTimeoutTicks) {
-            atomicExch(&ctr->stream_abort, 1u);
-            return kReplayNone;
-        }
-        __builtin_amdgcn_s_sleep(64);  // items arrive in bursts while the waves drain
-    }
-}
 RT_DEV uint32_t replay_claim(TraceCounters* ctr, const ReplayItem* list, uint32_t fast_grid) {
     const uint32_t i = atomicAdd(&ctr->replay_pull, 1u);
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
@@ -2593,8 +2409,8 @@ RT_DEV bool take_sample(ItemPool& pool, bool want, const DevCamera& C, const Dev
                 // The streaming replay keeps 1 + backlog / waves lanes of a wave busy: the
                 // replayed paths are few and long, and a wave's segment takes as long as its
                 // slowest lane, so they spread over the waves unless there are many.
-                uint32_t lim = Q.migrate ? 64u : 1u;  // handed-over paths are packed (kMigrateCap)
-                if (leader && !Q.migrate) {
+                uint32_t lim = 1u;
+                if (leader) {
                     const uint32_t n = __hip_atomic_load(&ctr->replay_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     const uint32_t pl = __hip_atomic_load(&ctr->replay_pull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     lim += (n > pl ? n - pl : 0u) / gridDim.x;
@@ -2603,17 +2419,7 @@ RT_DEV bool take_sample(ItemPool& pool, bool want, const DevCamera& C, const Dev
                 if (64u - (uint32_t)__popcll(need) >= lim) break;
             }
             if (leader) {
-                if (list && stream_grid && Q.migrate) {  // as many entries as idle lanes, or the backlog
-                    const uint32_t n = __hip_atomic_load(&ctr->replay_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    const uint32_t pl = __hip_atomic_load(&ctr->replay_pull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    const uint32_t backlog = n > pl ? n - pl : 0u, idle = (uint32_t)__popcll(need);
-                    cnt = backlog < idle ? backlog : idle;
-                    cnt = cnt < 1u ? 1u : cnt;
-                    bt = replay_claim_n(ctr, list, stream_grid, cnt);
-#ifdef RT_PROFILE_REGIONS
-                    role_event(bt);
-#endif
-                } else if (list && stream_grid) {  // the streaming replay: one entry per claim
+                if (list && stream_grid) {  // the streaming replay: one entry per claim
                     cnt = 1u;
                     bt = replay_claim(ctr, list, stream_grid);
 #ifdef RT_PROFILE_REGIONS
@@ -2648,21 +2454,11 @@ RT_DEV bool take_sample(ItemPool& pool, bool want, const DevCamera& C, const Dev
             uint32_t x, y, s, sl;
             if (list) {
                 const ReplayItem it = replay_take(list, pool.next + rank);
-                if (it.sample & kMigrated) {
-                    // a path a draining fast-kernel wave handed over: it continues where it stopped
-                    // (the record was written before the entry was published, behind a release)
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                    load_path(path_records(list) + (size_t)it.pixel * kPathRecordU4, slot, s_local, depth, g, L, T, ray);
-                    got = true;
-                    x = P.width;  // nothing to start below
-                    y = s = sl = 0u;
-                } else {
-                    y = it.pixel / P.width;
-                    x = it.pixel - y * P.width;
-                    s = it.sample;
-                    const uint32_t blk = (y >> 3) * P.blocks_x + (x >> 3);
-                    sl = ((blk - P.shard_index) / P.shard_count) * 64u + ((y & 7u) << 3) + (x & 7u);
-                }
+                y = it.pixel / P.width;
+                x = it.pixel - y * P.width;
+                s = it.sample;
+                const uint32_t blk = (y >> 3) * P.blocks_x + (x >> 3);
+                sl = ((blk - P.shard_index) / P.shard_count) * 64u + ((y & 7u) << 3) + (x & 7u);
             } else {
                 // unit pool.batch + (item >> 6); a batch (<= Q.group <= Q.samples units) crosses at
                 // most one block boundary, so the batch's block and sample are divided once
@@ -2983,40 +2779,6 @@ __global__ __launch_bounds__(64, kWaves) void trace_samples(DevScene Sg, DevCame
         }
         PROF_ADD(kPrRefill, pr);
         if (__ballot(has) == 0ull) break;  // pool exhausted and every path finished
-        if constexpr (kKind == 0) {
-            // The drain hand-over (kMigrateCap above): the pool is dry and few of this wave's
-            // paths are left, so they move to the streaming replay pass and the wave exits.
-            if (Q.migrate && pool.exhausted) {
-                const unsigned long long act = __ballot(has);
-                const uint32_t nact = (uint32_t)__popcll(act);
-                if (nact <= Q.migrate) {
-                    uint32_t mbase = kReplayNone, rbase = 0u;
-                    if (lane == 0u) {  // the whole wave is here (uniform control flow)
-                        mbase = atomicAdd(&ctr->migrate_count, nact);
-                        if (mbase + nact <= kMigrateCap)
-                            rbase = atomicAdd(&ctr->replay_count, nact);
-                        else
-                            mbase = kReplayNone;
-                    }
-                    mbase = __builtin_amdgcn_readfirstlane(mbase);
-                    rbase = __builtin_amdgcn_readfirstlane(rbase);
-                    // (a replay list that overflows is re-rendered whole by the serialized pass,
-                    // so lanes that could not publish just go on)
-                    if (mbase != kReplayNone && rbase + nact <= kReplayCap) {
-                        if (has) {
-                            const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32),
-                                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
-                            save_path(path_records(replay_list) + (size_t)(mbase + r) * kPathRecordU4, slot,
-                                      take_sample_idx, depth, g, L, T, ray);
-                            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-                            replay_publish(replay_list, rbase + r, mbase + r, kMigrated | take_sample_idx);
-                            has = false;
-                        }
-                        break;
-                    }
-                }
-            }
-        }
 #ifdef RT_PROFILE_REGIONS
         if (kKind == 0) {  // throughput histogram: this iteration's segments into the current bucket
             const uint32_t b = (uint32_t)((__builtin_amdgcn_s_memrealtime() - wave_t0) / kTpTicks);
@@ -3171,6 +2933,10 @@ __global__ void kat_eval(int op, const float* __restrict__ in, float* __restrict
     } else if (op == 2) {  // Sphere::get_uv (sphere.rs:41-46)
         const float* a = in + 3u * i;
         sphere_uv(mk(a[0], a[1], a[2]), r0, r1);
+    } else if (op == 4) {  // x / d through div_rn (the reciprocal RN(1/d), then Markstein's correction), and x / d
+        const float x = in[2u * i], d = in[2u * i + 1u];
+        r0 = div_rn(x, d, 1.0f / d);
+        r1 = x / d;
     } else if (op == 3) {  // Sphere::hit's root (sphere.rs:49-103): center, radius, origin, direction, t_min, t_max
         const float* a = in + 12u * i;
         Ray r;
@@ -3340,7 +3106,7 @@ TraceKernel fast_instance(int waves, uint32_t features) {
 }
 
 // rt_set_option's process-wide diagnostic switches (include/rt.h rt_option).
-std::atomic<int64_t> g_opt[RT_OPT_COUNT] = {{0}, {0}, {0}, {0}, {-1}, {0}, {0}, {0}, {-1}};
+std::atomic<int64_t> g_opt[RT_OPT_COUNT] = {{0}, {0}, {0}, {0}, {-1}, {0}, {0}, {0}};
 int64_t opt(int o) { return g_opt[o].load(std::memory_order_relaxed); }
 
 int check_device(int device) {
@@ -3786,9 +3552,7 @@ int rt_render_launch_camera(rt_scene_handle s, const rt_camera* camera, const rt
             return rthost::set_error(RT_ERR_OOM, std::string("hipMalloc counter: ") + hipGetErrorString(e));
     }
     if (!s->replay) {
-        // the list, then the drain hand-over's path records (kMigrateCap x 96 B)
-        if ((e = hipMalloc(&s->replay, sizeof(ReplayItem) * (size_t)kReplayCap +
-                                           sizeof(uint4) * kPathRecordU4 * (size_t)kMigrateCap)) != hipSuccess)
+        if ((e = hipMalloc(&s->replay, sizeof(ReplayItem) * (size_t)kReplayCap)) != hipSuccess)
             return rthost::set_error(RT_ERR_OOM, std::string("hipMalloc replay list: ") + hipGetErrorString(e));
         if ((e = hipMemsetAsync(s->replay, 0xff, sizeof(ReplayItem) * (size_t)kReplayCap, (hipStream_t)stream)) !=
             hipSuccess)  // every entry kReplayFree
@@ -3892,13 +3656,6 @@ int rt_render_launch_camera(rt_scene_handle s, const rt_camera* camera, const rt
         q.guide = 2u;  // measured on C3 (63 and 500 spp): 2 beats 4, 8, 16 and 32 (tools/session_guide.sh)
         if (const int64_t gd = opt(RT_OPT_GUIDE)) q.guide = (uint32_t)gd;  // diagnostics / A-B runs
         q.nslots = (uint32_t)nslots;
-        // the drain hand-over needs the streaming replay pass to resume the paths beside the fast
-        // kernel (the serialized pass would take them only after it): default 16 paths per wave
-        q.migrate = 0u;
-        if (!exact && !dev_ref.hrpp_tab && !(dp.tune & kModeReplayRef) && !(dp.tune & kModeNoStream)) {
-            const int64_t m = opt(RT_OPT_MIGRATE);
-            q.migrate = m < 0 ? kMigrateDefault : (uint32_t)m;
-        }
         if ((e = hipMemsetAsync(s->counter, 0, sizeof(TraceCounters), st)) != hipSuccess)
             return hip_fail(e, "memset counters");
         // the launch's camera behind the counters: the flat-list instances (kernel_flat.hip, RT_CAMMEM)
@@ -4178,7 +3935,6 @@ int rt_set_option(int option, int64_t value) {
         case RT_OPT_LAUNCH_LOG: ok = value == 0 || value == 1; break;
         case RT_OPT_BVH_BUILD: ok = value >= 0 && value <= 2; break;
         case RT_OPT_GUIDE: ok = value >= 0 && value <= 256; break;
-        case RT_OPT_MIGRATE: ok = value >= -1 && value <= 64; break;
     }
     if (!ok) return rthost::set_error(RT_ERR_INVALID, "option value out of range");
     g_opt[option].store(value, std::memory_order_relaxed);
@@ -4221,12 +3977,13 @@ int rt_scene_trace_time(rt_scene_handle s, double* total_ms, uint64_t* launches,
 int rt_device_kat(int op, const float* in, float* out, uint32_t n) {
     rthost::clear_error();
     if (!in || !out) return rthost::set_error(RT_ERR_INVALID, "NULL argument");
-    if (op < 0 || op > 3) return rthost::set_error(RT_ERR_INVALID, "unknown KAT op");
+    if (op < 0 || op > 4) return rthost::set_error(RT_ERR_INVALID, "unknown KAT op");
     int rc = check_device(0);
     if (rc) return rc;
     if (n == 0) return RT_OK;
     DeviceGuard g(0);
-    const size_t in_floats = (size_t)n * (op <= 1 ? 14u : (op == 2 ? 3u : 12u)), out_floats = (size_t)n * 2u;
+    const size_t in_floats = (size_t)n * (op <= 1 ? 14u : (op == 2 ? 3u : (op == 4 ? 2u : 12u))),
+                 out_floats = (size_t)n * 2u;
     float *din = nullptr, *dout = nullptr;
     hipError_t e = hipMalloc(&din, in_floats * sizeof(float));
     if (e == hipSuccess) e = hipMalloc(&dout, out_floats * sizeof(float));

@@ -775,10 +775,6 @@ class Lowerer {
         };
         std::vector<std::vector<Slot>> wide;  // per wide node, in DFS preorder
         std::vector<uint32_t> wide_depth;
-        // per wide node: the axis along which its BVH2 node's two children's centres differ most
-        // (Bvh::new's split axis for the trees it builds), kept in an interior node's rank[0]
-        // (unused there: its slots are nodes); read only by the RT_EXP_NOSORT=2 experiment
-        std::vector<uint32_t> wide_axis;
         std::function<uint32_t(uint32_t, uint32_t)> build4 = [&](uint32_t x, uint32_t depth) -> uint32_t {
             std::vector<Slot> sl;
             for (int k = 0; k < 2; ++k) {
@@ -802,19 +798,6 @@ class Lowerer {
             uint32_t me = (uint32_t)wide.size();
             wide.push_back({});
             wide_depth.push_back(depth);
-            {
-                uint32_t ax = 0u;
-                if (tn[x].is_node[0] && tn[x].is_node[1]) {
-                    const Box& a = tn[tn[x].child[0]].box;
-                    const Box& b = tn[tn[x].child[1]].box;
-                    const float d[3] = {std::fabs((b.mn.x + b.mx.x) - (a.mn.x + a.mx.x)),
-                                        std::fabs((b.mn.y + b.mx.y) - (a.mn.y + a.mx.y)),
-                                        std::fabs((b.mn.z + b.mx.z) - (a.mn.z + a.mx.z))};
-                    ax = d[1] > d[0] ? 1u : 0u;
-                    if (d[2] > d[ax]) ax = 2u;
-                }
-                wide_axis.push_back(ax);
-            }
             for (Slot& c : sl)
                 if (c.node) c.id = build4(c.id, depth + 1) | 0x40000000u;  // mark: wide index (remapped below)
             wide[me] = sl;
@@ -868,7 +851,7 @@ class Lowerer {
                 if (c.node) return false;
             return true;
         };
-        auto put = [&](uint32_t o, const std::vector<Slot>& sl, uint32_t flags, uint32_t axis = 0u) {
+        auto put = [&](uint32_t o, const std::vector<Slot>& sl, uint32_t flags) {
             float mnx[4], mny[4], mnz[4], mxx[4], mxy[4], mxz[4];
             uint32_t ch[4], rk[4];
             for (uint32_t k = 0; k < 4; ++k) {
@@ -889,7 +872,6 @@ class Lowerer {
                 rk[k] = have ? sl[k].rank : 0u;
             }
             rk[3] |= flags;
-            if (!sl.empty() && sl[0].node) rk[0] = axis;  // interior node (all slots are nodes)
             rtdev::f4* n = &s_->nodes[(size_t)o * rtdev::kBvhNodeF4];
             n[0] = {mnx[0], mnx[1], mnx[2], mnx[3]};
             n[1] = {mny[0], mny[1], mny[2], mny[3]};
@@ -934,7 +916,7 @@ class Lowerer {
         }
         uint32_t max_wide_depth = 0;
         for (uint32_t w = 0; w < wide.size(); ++w) {
-            put(base + 1 + w, wide[w], 0u, wide_axis[w]);
+            put(base + 1 + w, wide[w], 0u);
             max_wide_depth = std::max(max_wide_depth, wide_depth[w]);
         }
         // a BVH4 visit pushes at most kBvhWidth - 1 siblings per level (2 words

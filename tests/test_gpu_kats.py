@@ -67,3 +67,29 @@ def test_random_sphere_uv_device_equals_oracle(rt, orc):
     got = rt.device_kat(2, p)
     want = np.array([orc.sphere_uv(q) for q in p], dtype=np.float32)
     np.testing.assert_array_equal(got, want)
+
+
+def test_division_from_the_reciprocal_is_correctly_rounded(rt):
+    # div_rn (kernel.hip): x / d from RN(1/d) and Markstein's correction inside the gate, the
+    # compiler's division outside it. The exhaustive significand check is tools/markstein_check.hip
+    # (profiles/r05/markstein_check.log); here random operands over the whole exponent range, the
+    # gate's edges and the special values, against numpy's correctly rounded f32 division.
+    rng = np.random.default_rng(11)
+    n = 1 << 20
+    bits = rng.integers(0, 1 << 32, size=(n, 2), dtype=np.uint64).astype(np.uint32)
+    cases = [bits.view(np.float32)]
+    mant = rng.integers(0, 1 << 23, size=(n, 2), dtype=np.uint32)
+    expo = rng.integers(127 - 70, 127 + 70, size=(n, 2), dtype=np.uint32)
+    cases.append(((expo << 23) | mant).view(np.float32) * np.where(rng.random((n, 2)) < 0.5, -1, 1).astype(np.float32))
+    edge = np.array([0.0, -0.0, 2.0 ** -60, -(2.0 ** -60), 2.0 ** 60, 2.0 ** -61, 2.0 ** 61, 1e-45, 1e-40, 3e38,
+                     np.inf, -np.inf, np.nan, 1.0, -1.0, 3.0, 0.1, 555.0], dtype=np.float32)
+    cases.append(np.array(np.meshgrid(edge, edge)).reshape(2, -1).T.astype(np.float32))
+    a = np.concatenate(cases)
+    out = rt.device_kat(4, a)
+    with np.errstate(all="ignore"):
+        want = (a[:, 0] / a[:, 1]).astype(np.float32)
+    # the device's own division and div_rn against the host, bit for bit (NaN payloads aside)
+    for col in (1, 0):
+        got = out[:, col]
+        same = (got.view(np.uint32) == want.view(np.uint32)) | (np.isnan(got) & np.isnan(want))
+        assert same.all(), (col, a[~same][:5], got[~same][:5], want[~same][:5])

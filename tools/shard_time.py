@@ -21,6 +21,9 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--spp", type=int, default=None, help="override the config's samples per pixel")
     ap.add_argument("--shard-only", action="store_true", help="skip the whole-frame (1-rank) reference run")
+    ap.add_argument("--pipeline", action="store_true",
+                    help="two frames in flight (bench.py --pipeline on): alternate two scene handles and streams "
+                         "and report the steady-state time per step")
     a = ap.parse_args()
     import torch
     import raytracinginoneweekendinrust_amd as rt
@@ -33,6 +36,27 @@ def main():
     scene = rt.Scene.generate(cfg.scene, cfg.scene_seed)
     ds = rt.DeviceScene(scene)
     out = torch.zeros(cfg.width * cfg.height * 3, dtype=torch.float32, device="cuda")
+    if a.pipeline:
+        ds2 = rt.DeviceScene(scene)
+        out2 = torch.zeros_like(out)
+        st = [torch.cuda.Stream(), torch.cuda.Stream()]
+        for n in ([a.n] if a.shard_only else sorted({1, a.n})):
+            p = rt.render_params(cfg.width, cfg.height, cfg.spp, cfg.depth, background=cfg.background(),
+                                 seed=cfg.render_seed, shard_index=a.rank if n > 1 else 0, shard_count=n)
+            for k in range(2):  # warm-up
+                (ds, ds2)[k % 2].launch(cfg.camera(), p, (out, out2)[k % 2].data_ptr(), 0, st[k % 2].cuda_stream)
+            torch.cuda.synchronize()
+            import time
+            t0 = time.perf_counter()
+            for k in range(a.reps):
+                (ds, ds2)[k % 2].launch(cfg.camera(), p, (out, out2)[k % 2].data_ptr(), 0, st[k % 2].cuda_stream)
+            torch.cuda.synchronize()
+            ms = (time.perf_counter() - t0) * 1e3 / a.reps
+            print(f"{cfg.name} shard {a.rank if n > 1 else 0}/{n}: pipelined step {ms:.2f} ms "
+                  f"({a.reps} frames, two in flight)", flush=True)
+        ds2.close()
+        ds.close()
+        return
     for n in ([a.n] if a.shard_only else sorted({1, a.n})):
         p = rt.render_params(cfg.width, cfg.height, cfg.spp, cfg.depth, background=cfg.background(),
                              seed=cfg.render_seed, shard_index=a.rank if n > 1 else 0, shard_count=n)
