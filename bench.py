@@ -99,7 +99,7 @@ def cpu_threads() -> int:
     return max(1, n)
 
 
-PMC_DIRS = (os.path.join(ROOT, "profiles", "r04"), os.path.join(ROOT, "profiles", "r03"), os.path.join(ROOT, "profiles"))
+PMC_DIRS = tuple(os.path.join(ROOT, "profiles", d) for d in ("r05", "r04", "r03", ""))
 
 
 def library_md5() -> str:

@@ -422,9 +422,9 @@ int rt_device_numeric_eval(int op, const double* a, const double* b, double* out
  * four-child test — in: 14 floats per case (min[3], max[3], origin[3], direction[3],
  * t_min, t_max), out: (hit 1/0, entry t); op 2: Sphere::get_uv (sphere.rs:41-46) —
  * in: p[3], out: (u, v); op 3: Sphere::hit's root (sphere.rs:49-103) — in: center[3],
- * radius, origin[3], direction[3], t_min, t_max, out: (hit 1/0, t); op 4: the division
- * from a correctly rounded reciprocal the kernel uses for a medium's cube sides — in: x, d,
- * out: (div_rn(x, d, 1/d), x / d). */
+ * radius, origin[3], direction[3], t_min, t_max, out: (hit 1/0, t); op 4: a cube side's
+ * quotient (k - o) / d as a BVH cube leaf forms it from the ray's reciprocal (in range: RN(1/d) and
+ * Markstein's correction; otherwise the division) — in: k, o, d, out: (that quotient, (k - o) / d). */
 int rt_device_kat(int op, const float* in, float* out, uint32_t n);
 
 #ifdef __cplusplus

@@ -159,6 +159,9 @@ struct DevScene {
     uint32_t* stack_spill;
     uint32_t spill_depth;
     uint32_t num_nodes;   // BVH4 nodes (the audit build bounds-checks every visited index)
+    // Every rect / cube-side coordinate is +0 or of magnitude in [2^-20, 2^20] (set at upload): a
+    // cube leaf's side quotients may then come from the ray's reciprocals (kernel.hip div_rn_safe).
+    uint32_t rect_rcp_ok;
 };
 
 // Camera::new (camera.rs:44-81) evaluated on the host.

@@ -543,32 +543,37 @@ RT_DEV bool msphere_t(f4 m0, f4 m1, f4 m2, const Ray& r, float tmin, float tmax,
 }
 
 // Division from a correctly rounded reciprocal (Markstein): with inv = RN(1/d), q0 = RN(x * inv),
-// r = fma(-d, q0, x) (exact) and q = RN(q0 + r * inv) equals RN(x / d) whenever nothing under- or
-// overflows. Checked exhaustively over all 2^46 pairs of f32 significands (tools/markstein_check.hip,
-// profiles/r05/markstein_check.log: 0 mismatches); scaling x and d by powers of two scales every
-// step exactly, so the check covers every input the gate admits: |x| and |q0| in [2^-60, 2^60]
-// (then |d| and inv lie in [2^-121, 2^121] and r, r * inv are normal or r is 0). Anything else
-// (zeros, denormals, infinities, NaN, extreme ratios) takes the compiler's division.
-#ifndef RT_MARKSTEIN
-#define RT_MARKSTEIN 1
+// r = fma(-d, q0, x) (exact) and q = RN(q0 + r * inv) equals RN(x / d) whenever no intermediate under-
+// or overflows and r is representable. Checked exhaustively over all 2^46 pairs of f32 significands
+// (tools/markstein_check.hip, profiles/r05/markstein_check.log: 0 mismatches); scaling x and d by
+// powers of two scales every step exactly. A cube leaf inside a BVH traversal has the ray's
+// reciprocals at hand (bvh_hit's inv): when the scene's rect coordinates k (S.rect_rcp_ok) and the
+// ray's origin components are +-0 or of magnitude in [2^-20, 2^20] and its direction components are
+// in that range (rcp_ray_ok), x = k - o is 0 (never -0: no coordinate is -0) or of magnitude in
+// [2^-43, 2^21], q0 lies in [2^-63, 2^41] or is a zero of the right sign, and r = x - d q0 is a
+// multiple of at least 2^-149, hence exact: every side quotient is the reference's division.
+#ifndef RT_MARKSTEIN_CUBE
+#define RT_MARKSTEIN_CUBE 1
 #endif
-RT_DEV bool div_gate(float v) {  // |v| in [2^-60, 2^60], NaN excluded
-    return (__float_as_uint(v) & 0x7fffffffu) - 0x21800000u <= 0x5d800000u - 0x21800000u;
+RT_DEV bool rcp_range(float v) {  // |v| in [2^-20, 2^20]
+    return (__float_as_uint(v) & 0x7fffffffu) - 0x35800000u <= 0x49800000u - 0x35800000u;
 }
-RT_DEV float div_rn(float x, float d, float inv) {
-    const float q0 = x * inv;
-    if (div_gate(x) && div_gate(q0)) return __builtin_fmaf(__builtin_fmaf(-d, q0, x), inv, q0);
-    return x / d;
+RT_DEV bool rcp_ray_ok(const Ray& r) {
+    const auto zero = [](float v) { return (__float_as_uint(v) & 0x7fffffffu) == 0u; };
+    return rcp_range(r.d.x) && rcp_range(r.d.y) && rcp_range(r.d.z) && (zero(r.o.x) || rcp_range(r.o.x)) &&
+           (zero(r.o.y) || rcp_range(r.o.y)) && (zero(r.o.z) || rcp_range(r.o.z));
 }
-// side_t with the direction component's reciprocal at hand (cube sides of a BVH leaf, a medium's
-// cube): the same quotient through div_rn.
-RT_DEV bool side_t_inv(float k, float ok, float dk, float dinv, float oa, float da, float ob, float db, float a0,
+RT_DEV float rcp_quotient(float k, float ok, float dk, float dinv) {  // (k - ok) / dk under the gate above
+    const float x = k - ok, q0 = x * dinv;
+    return __builtin_fmaf(__builtin_fmaf(-dk, q0, x), dinv, q0);
+}
+RT_DEV bool side_t_rcp(float k, float ok, float dk, float dinv, float oa, float da, float ob, float db, float a0,
                        float a1, float b0, float b1, float tmin, float tmax, float& t) {
-    const float tt = div_rn(k - ok, dk, dinv);
+    const float tt = rcp_quotient(k, ok, dk, dinv);
     if (tt < tmin || tt > tmax) return false;
-    const float x = oa + tt * da;
-    const float y = ob + tt * db;
-    if (x < a0 || x > a1 || y < b0 || y > b1) return false;
+    const float xx = oa + tt * da;
+    const float yy = ob + tt * db;
+    if (xx < a0 || xx > a1 || yy < b0 || yy > b1) return false;
     t = tt;
     return true;
 }
@@ -680,33 +685,13 @@ RT_DEV bool leaf_hit(const DevScene& S, uint32_t code, const Ray& r, const RayD&
         const float ox = r.o.x, oy = r.o.y, oz = r.o.z, dx = r.d.x, dy = r.d.y, dz = r.d.z;
         bool any = false;
         uint32_t face = 0u;
-        if constexpr (kInv && RT_MARKSTEIN) {  // the BVH traversal's reciprocals: no division per side
-            // the six quotients from the reciprocals (div_rn), one rare branch back to the divisions
-            float q[6] = {(z0 - oz) * inv.z, (z1 - oz) * inv.z, (y0 - oy) * inv.y,
-                          (y1 - oy) * inv.y, (x0 - ox) * inv.x, (x1 - ox) * inv.x};
-            const float num[6] = {z0 - oz, z1 - oz, y0 - oy, y1 - oy, x0 - ox, x1 - ox};
-            const float den[6] = {dz, dz, dy, dy, dx, dx}, rcp[6] = {inv.z, inv.z, inv.y, inv.y, inv.x, inv.x};
-            bool ok = true;
-#pragma unroll
-            for (int f = 0; f < 6; ++f) ok = ok && div_gate(num[f]) && div_gate(q[f]);
-            if (ok) {
-#pragma unroll
-                for (int f = 0; f < 6; ++f) q[f] = __builtin_fmaf(__builtin_fmaf(-den[f], q[f], num[f]), rcp[f], q[f]);
-            } else {
-#pragma unroll
-                for (int f = 0; f < 6; ++f) q[f] = num[f] / den[f];
-            }
-            auto side_q = [&](float tt, float oa, float da, float ob, float db, float a0, float a1, float b0, float b1) {
-                if (tt < tmin || tt > closest) return false;
-                const float x = oa + tt * da, y = ob + tt * db;
-                return !(x < a0 || x > a1 || y < b0 || y > b1);
-            };
-            if (side_q(q[0], ox, dx, oy, dy, x0, x1, y0, y1)) { closest = q[0]; face = 0u; any = true; }
-            if (side_q(q[1], ox, dx, oy, dy, x0, x1, y0, y1)) { closest = q[1]; face = 1u; any = true; }
-            if (side_q(q[2], ox, dx, oz, dz, x0, x1, z0, z1)) { closest = q[2]; face = 2u; any = true; }
-            if (side_q(q[3], ox, dx, oz, dz, x0, x1, z0, z1)) { closest = q[3]; face = 3u; any = true; }
-            if (side_q(q[4], oy, dy, oz, dz, y0, y1, z0, z1)) { closest = q[4]; face = 4u; any = true; }
-            if (side_q(q[5], oy, dy, oz, dz, y0, y1, z0, z1)) { closest = q[5]; face = 5u; any = true; }
+        if (kInv && RT_MARKSTEIN_CUBE && S.rect_rcp_ok && rcp_ray_ok(r)) {  // the ray's reciprocals (side_t_rcp)
+            if (side_t_rcp(z0, oz, dz, inv.z, ox, dx, oy, dy, x0, x1, y0, y1, tmin, closest, t)) { closest = t; face = 0u; any = true; }
+            if (side_t_rcp(z1, oz, dz, inv.z, ox, dx, oy, dy, x0, x1, y0, y1, tmin, closest, t)) { closest = t; face = 1u; any = true; }
+            if (side_t_rcp(y0, oy, dy, inv.y, ox, dx, oz, dz, x0, x1, z0, z1, tmin, closest, t)) { closest = t; face = 2u; any = true; }
+            if (side_t_rcp(y1, oy, dy, inv.y, ox, dx, oz, dz, x0, x1, z0, z1, tmin, closest, t)) { closest = t; face = 3u; any = true; }
+            if (side_t_rcp(x0, ox, dx, inv.x, oy, dy, oz, dz, y0, y1, z0, z1, tmin, closest, t)) { closest = t; face = 4u; any = true; }
+            if (side_t_rcp(x1, ox, dx, inv.x, oy, dy, oz, dz, y0, y1, z0, z1, tmin, closest, t)) { closest = t; face = 5u; any = true; }
         } else {
             if (side_t(z0, oz, dz, ox, dx, oy, dy, x0, x1, y0, y1, tmin, closest, t)) { closest = t; face = 0u; any = true; }
             if (side_t(z1, oz, dz, ox, dx, oy, dy, x0, x1, y0, y1, tmin, closest, t)) { closest = t; face = 1u; any = true; }
@@ -1369,7 +1354,9 @@ RT_DEV bool bvh_run(const DevScene& S, float delta, const f4* wrapper, const Ray
                     const RayD q = to_d(r);  // f64 ray for sphere leaves, rebuilt here rather than kept live
                     ABLATE(kAbLeaf2, float c2 = c; uint32_t h2 = 0u;
                            if (leaf_hit<kF>(S, lcode, r, q, tmin, c2, h2) && h2 == 0x7fffffffu) c = -1.0f;);
-                    if (leaf_hit<kF>(S, lcode, r, q, tmin, c, code)) {
+                    // cube sides from the ray's reciprocals (side_t_rcp) except in the triangle preset,
+                    // whose instance lost 1.6% to the extra code (C3 +2%; uniform_entries_ab.log)
+                    if (leaf_hit<kF, (kF & kFTri) == 0u>(S, lcode, r, q, tmin, c, code, inv)) {
                         // cube faces rank + 0..5 (the face leaf_hit's list walk kept)
                         const uint32_t rk = rank + (rtdev::leaf_type(lcode) == rtdev::kLeafCube
                                                         ? rtdev::leaf_index(code) - rtdev::leaf_index(lcode)
@@ -1546,25 +1533,23 @@ RT_DEV void spheres_surely_missed2(f4 s0, f4 s1, const Ray& r, float a, bool& m0
     m1 = m[1] > 0x1p-100f && disc[1] < lim[1];
 }
 
-#ifndef RT_EXP_UNIFORM_RECT
-#define RT_EXP_UNIFORM_RECT 1
-#endif
-#ifndef RT_EXP_UNIFORM_ENTRY
-#define RT_EXP_UNIFORM_ENTRY 1
-#endif
-// A top-level entry's record is the same for every lane of the wave (the list walk is a
-// wave-uniform loop): its fields are read once into scalar registers (readfirstlane), so the
-// wave branches on them instead of masking lanes.
+// A top-level entry's record is the same for every lane of the wave (the list walk is a wave-uniform
+// loop). In the triangle-BVH and flat-list presets its fields are read once into scalar registers
+// (readfirstlane), so the wave branches on them instead of masking lanes, and a top-level rectangle's
+// plane axis picks one of three code paths instead of every lane selecting the ray components per
+// axis. Measured (same box, bit-identical, profiles/r05/experiments/uniform_entries_ab.log): C4 +3.5%,
+// C5 +0.8%; C3 -1% and C2 -4% (register allocation), so their presets keep the vector reads.
+template <uint32_t kF>
+constexpr bool kUniformEntries = (kF & kFTri) != 0u || (kF & (kFBvh | kFRuns)) == 0u;
+template <uint32_t kF>
 RT_DEV uint32_t uni(uint32_t v) {
-#if RT_EXP_UNIFORM_ENTRY
-    return __builtin_amdgcn_readfirstlane(v);
-#else
+    if constexpr (kUniformEntries<kF>) return __builtin_amdgcn_readfirstlane(v);
     return v;
-#endif
 }
 // apply_op for a wave-uniform transform record: the Translate / RotateY choice is a scalar branch.
+template <uint32_t kF>
 RT_DEV Ray apply_op_u(f4 op, Ray r) {
-    if (__uint_as_float(uni(__float_as_uint(op.w))) == 0.0f) {
+    if (__uint_as_float(uni<kF>(__float_as_uint(op.w))) == 0.0f) {
         r.o = r.o - xyz(op);
     } else {
         float s = op.x, c = op.y;
@@ -1580,11 +1565,11 @@ constexpr uint32_t kRunPretestMin = 8u;  // sphere runs at least this long take 
 template <int kKind, uint32_t kF>
 RT_DEV bool entry_geom_hit(const DevScene& S, float delta, const DevEntry* E, Ray r, float tmin, float& closest,
                            uint32_t& hit_code, uint32_t* stk, uint32_t mode, bool& replay) {
-    uint32_t ntf = uni(E->ntf);
-    for (uint32_t i = 0; i < ntf; ++i) r = apply_op_u(E->tf[i], r);
-    const uint32_t kind = uni(E->kind);
+    uint32_t ntf = uni<kF>(E->ntf);
+    for (uint32_t i = 0; i < ntf; ++i) r = apply_op_u<kF>(E->tf[i], r);
+    const uint32_t kind = uni<kF>(E->kind);
     if (kind == rtdev::kEntSphereRun) {  // consecutive top-level spheres, in list order
-        const uint32_t first = uni(E->payload), n = uni(E->pad[0]);
+        const uint32_t first = uni<kF>(E->payload), n = uni<kF>(E->pad[0]);
         const RayD q = to_d(r);
         const bool pretest = (kF & kFRuns) && n >= kRunPretestMin && !(mode & kModeNoPretest);  // long lists (random_spheres without a BVH): most spheres are misses
         bool any = false;
@@ -1626,11 +1611,10 @@ RT_DEV bool entry_geom_hit(const DevScene& S, float delta, const DevEntry* E, Ra
             ABLATE(kAbBvh2, float c2 = closest; uint32_t h2 = 0u; bool rp = false;
                    if (bvh_hit<kKind, kF>(S, delta, E->payload, r, tmin, c2, h2, stk, mode, rp) && h2 == 0x7fffffffu)
                        closest = -1.0f;);
-            return bvh_hit<kKind, kF>(S, delta, uni(E->payload), r, tmin, closest, hit_code, stk, mode, replay);
+            return bvh_hit<kKind, kF>(S, delta, uni<kF>(E->payload), r, tmin, closest, hit_code, stk, mode, replay);
         }
     }
-#if RT_EXP_UNIFORM_RECT
-    {
+    if constexpr (kUniformEntries<kF>) {
         // A top-level rectangle (walls, lights): its record is the same for the whole wave, so its
         // plane axis is read once (readfirstlane) and the wave branches on it, instead of every lane
         // selecting the six ray components per axis (rect_axes). Same operations as rect_t.
@@ -1654,11 +1638,10 @@ RT_DEV bool entry_geom_hit(const DevScene& S, float delta, const DevEntry* E, Ra
             return h;
         }
     }
-#endif
     RayD q = to_d(r);
     ABLATE(kAbGeom2, float c2 = closest; uint32_t h2 = 0u;
            if (leaf_hit<kF | kFLeafRM>(S, E->payload, r, q, tmin, c2, h2) && h2 == 0x7fffffffu) closest = -1.0f;);
-    return leaf_hit<kF | kFLeafRM>(S, uni(E->payload), r, q, tmin, closest, hit_code);  // top level: any primitive
+    return leaf_hit<kF | kFLeafRM>(S, uni<kF>(E->payload), r, q, tmin, closest, hit_code);  // top level: any primitive
 }
 
 // ConstantMedium::hit (hittable.rs:176-233); draws one U(0,1) once the clamped
@@ -1666,17 +1649,17 @@ RT_DEV bool entry_geom_hit(const DevScene& S, float delta, const DevEntry* E, Ra
 template <int kKind, uint32_t kF>
 RT_DEV bool medium_hit(const DevScene& S, float delta, const DevEntry* E, Ray r, float tmin, float tmax, Rng& g,
                        const Key& k, float& t_out, uint32_t* stk, uint32_t mode, bool& replay) {
-    uint32_t ntf = uni(E->ntf);
-    for (uint32_t i = 0; i < ntf; ++i) r = apply_op_u(E->tf[i], r);
-    const DevEntry* B = S.entries + uni(E->payload);
+    uint32_t ntf = uni<kF>(E->ntf);
+    for (uint32_t i = 0; i < ntf; ++i) r = apply_op_u<kF>(E->tf[i], r);
+    const DevEntry* B = S.entries + uni<kF>(E->payload);
     float t1 = kInf, t2 = kInf;
-    const uint32_t bkind = uni(B->kind), bcode = uni(B->payload);
+    const uint32_t bkind = uni<kF>(B->kind), bcode = uni<kF>(B->payload);
     if (bkind == rtdev::kEntGeom && rtdev::leaf_type(bcode) == rtdev::kLeafSphere) {
         // boundary.hit(-inf, inf) then boundary.hit(t1 + 1e-4, inf) on one sphere:
         // the same two roots, selected against two intervals.
         Ray rb = r;
-        uint32_t bn = uni(B->ntf);
-        for (uint32_t i = 0; i < bn; ++i) rb = apply_op_u(B->tf[i], rb);
+        uint32_t bn = uni<kF>(B->ntf);
+        for (uint32_t i = 0; i < bn; ++i) rb = apply_op_u<kF>(B->tf[i], rb);
         Roots R = sphere_roots(ld4(S.sph + rtdev::leaf_index(bcode)), to_d(rb));
         ABLATE(kAbMedium2, Roots R2 = sphere_roots(ld4(S.sph + rtdev::leaf_index(B->payload)), to_d(rb));
                if (R2.r1 == -1.0) t1 = -1.0f;);
@@ -1690,8 +1673,8 @@ RT_DEV bool medium_hit(const DevScene& S, float delta, const DevEntry* E, Ray r,
         // same bits). Left out of the triangle preset, whose scenes have no cube media and
         // whose register allocation the unused code cost 2.7% (C4).
         Ray rb = r;
-        uint32_t bn = uni(B->ntf);
-        for (uint32_t i = 0; i < bn; ++i) rb = apply_op_u(B->tf[i], rb);
+        uint32_t bn = uni<kF>(B->ntf);
+        for (uint32_t i = 0; i < bn; ++i) rb = apply_op_u<kF>(B->tf[i], rb);
         const uint32_t idx = rtdev::leaf_index(bcode);
         const f4 s0 = ld4(S.rect + 2 * idx);
         const float y1 = ld2(S.rect + 2 * idx + 1, 0).x, z1 = ld2(S.rect + 2 * idx + 5, 0).x;
@@ -1700,32 +1683,12 @@ RT_DEV bool medium_hit(const DevScene& S, float delta, const DevEntry* E, Ray r,
         float tt[6];
         uint32_t in = 0u;  // bit f: side f's point lies inside its rectangle (rectangle.rs:36-65)
         {
+            // (the six quotients from three reciprocals, div_rn, measured C5 -6%: kept as divisions;
+            // profiles/r05/experiments/uniform_entries_ab.log)
             const float num[6] = {z0 - oz, z1 - oz, y0 - oy, y1 - oy, x0 - ox, x1 - ox};
             const float den[6] = {dz, dz, dy, dy, dx, dx};
-            if constexpr (RT_MARKSTEIN && (kF & (kFBvh | kFRuns)) == 0u) {
-            // three reciprocals (the reference divides by each direction component twice), the six
-            // quotients from them (div_rn), one rare branch back to the divisions; the flat-list
-            // preset only (C5's smoke boxes): in the others the extra live values cost spilled
-            // registers (C3's instance 20 -> 32 VGPRs, C2's 19 -> 25) for code they rarely run
-            const float ix = 1.0f / dx, iy = 1.0f / dy, iz = 1.0f / dz;
-            const float rcp[6] = {iz, iz, iy, iy, ix, ix};
-            bool ok = true;
 #pragma unroll
-            for (int f = 0; f < 6; ++f) {
-                tt[f] = num[f] * rcp[f];
-                ok = ok && div_gate(num[f]) && div_gate(tt[f]);
-            }
-            if (ok) {
-#pragma unroll
-                for (int f = 0; f < 6; ++f) tt[f] = __builtin_fmaf(__builtin_fmaf(-den[f], tt[f], num[f]), rcp[f], tt[f]);
-            } else {
-#pragma unroll
-                for (int f = 0; f < 6; ++f) tt[f] = num[f] / den[f];
-            }
-            } else {
-#pragma unroll
-                for (int f = 0; f < 6; ++f) tt[f] = num[f] / den[f];
-            }
+            for (int f = 0; f < 6; ++f) tt[f] = num[f] / den[f];
         }
         auto side = [&](int f, float oa, float da, float ob, float db, float a0, float a1, float b0, float b1) {
             const float x = oa + tt[f] * da, y = ob + tt[f] * db;
@@ -2202,7 +2165,7 @@ RT_DEV bool world_hit(const DevScene& S, float delta, const Ray& r, Rng& g, cons
     for (uint32_t e = 0; e < S.num_top; ++e) {
         const DevEntry* E = S.entries + e;
         PROF_T0(pe);
-        if (uni(E->kind) == rtdev::kEntMedium) {
+        if (uni<kF>(E->kind) == rtdev::kEntMedium) {
             float t;
             if (medium_hit<kKind, kF>(S, delta, E, r, 0.001f, closest, g, k, t, stk, mode, replay)) {
                 closest = t;
@@ -2247,7 +2210,7 @@ RT_DEV void world_walk(const DevScene& S, float delta, const Ray& ray, Rng& g, c
         if (!(active && w.pos == e)) continue;
         PROF_T0(pe);
         const DevEntry* E = S.entries + e;
-        const uint32_t kind = uni(E->kind);
+        const uint32_t kind = uni<kF>(E->kind);
         if (kind == rtdev::kEntMedium) {
             float t;
             if (medium_hit<0, kF>(S, delta, E, ray, 0.001f, w.closest, g, k, t, stk, mode, replay)) {
@@ -2259,9 +2222,9 @@ RT_DEV void world_walk(const DevScene& S, float delta, const Ray& ray, Rng& g, c
             w.pos = e + 1u;
         } else if ((kF & kFBvh) && kind == rtdev::kEntBvh) {
             Ray r = ray;
-            const uint32_t ntf = uni(E->ntf);
-            for (uint32_t i = 0; i < ntf; ++i) r = apply_op_u(E->tf[i], r);
-            const uint32_t root = uni(E->payload);
+            const uint32_t ntf = uni<kF>(E->ntf);
+            for (uint32_t i = 0; i < ntf; ++i) r = apply_op_u<kF>(E->tf[i], r);
+            const uint32_t root = uni<kF>(E->payload);
             const f4* wrapper = S.nodes + (size_t)root * rtdev::kBvhNodeF4;
             const V inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
             if (!w.resume) {  // bvh_hit's hand-over rule (NaN-prone rays go to the reference kernel)
@@ -2933,10 +2896,12 @@ __global__ void kat_eval(int op, const float* __restrict__ in, float* __restrict
     } else if (op == 2) {  // Sphere::get_uv (sphere.rs:41-46)
         const float* a = in + 3u * i;
         sphere_uv(mk(a[0], a[1], a[2]), r0, r1);
-    } else if (op == 4) {  // x / d through div_rn (the reciprocal RN(1/d), then Markstein's correction), and x / d
-        const float x = in[2u * i], d = in[2u * i + 1u];
-        r0 = div_rn(x, d, 1.0f / d);
-        r1 = x / d;
+    } else if (op == 4) {  // a cube side's (k - o) / d the way a BVH cube leaf forms it, and the division
+        const float kk = in[3u * i], o = in[3u * i + 1u], d = in[3u * i + 2u];
+        const auto zero = [](float v) { return (__float_as_uint(v) & 0x7fffffffu) == 0u; };
+        const bool gate = (__float_as_uint(kk) == 0u || rcp_range(kk)) && (zero(o) || rcp_range(o)) && rcp_range(d);
+        r0 = gate ? rcp_quotient(kk, o, d, 1.0f / d) : (kk - o) / d;
+        r1 = (kk - o) / d;
     } else if (op == 3) {  // Sphere::hit's root (sphere.rs:49-103): center, radius, origin, direction, t_min, t_max
         const float* a = in + 12u * i;
         Ray r;
@@ -3245,6 +3210,16 @@ int rt_scene_upload(const rt_scene_desc* desc, int device, rt_scene_handle* out)
     d.hrpp_nkeys = (uint32_t)hs.hrpp_keys.size();
     d.hrpp_npred = hs.num_predictors;
     s->coord_bound = hs.coord_bound;
+    d.rect_rcp_ok = 1u;  // div_rn_safe's scene half: rect / cube-side coordinates +0 or in [2^-20, 2^20]
+    for (size_t i = 0; i + 1 < hs.rect.size(); i += 2) {  // (k, a0, a1, b0) (b1, axis, mat, 0)
+        const rtdev::f4 r0 = hs.rect[i], r1 = hs.rect[i + 1];
+        for (float c : {r0.x, r0.y, r0.z, r0.w, r1.x}) {
+            uint32_t b;
+            memcpy(&b, &c, 4);
+            const float a = std::fabs(c);
+            if (!(b == 0u || (a >= 0x1p-20f && a <= 0x1p20f))) d.rect_rcp_ok = 0u;
+        }
+    }
     s->features = (hs.tri.empty() ? 0u : kFTri) | (hs.bvh_rect_msph ? kFLeafRM : 0u);
     for (const rtdev::DevTexture& t : hs.texs)
         if (t.kind == rtdev::kTexMarble) s->features |= kFMarble;
@@ -3982,7 +3957,7 @@ int rt_device_kat(int op, const float* in, float* out, uint32_t n) {
     if (rc) return rc;
     if (n == 0) return RT_OK;
     DeviceGuard g(0);
-    const size_t in_floats = (size_t)n * (op <= 1 ? 14u : (op == 2 ? 3u : (op == 4 ? 2u : 12u))),
+    const size_t in_floats = (size_t)n * (op <= 1 ? 14u : (op == 2 || op == 4 ? 3u : 12u)),
                  out_floats = (size_t)n * 2u;
     float *din = nullptr, *dout = nullptr;
     hipError_t e = hipMalloc(&din, in_floats * sizeof(float));

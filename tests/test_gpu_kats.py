@@ -69,27 +69,35 @@ def test_random_sphere_uv_device_equals_oracle(rt, orc):
     np.testing.assert_array_equal(got, want)
 
 
-def test_division_from_the_reciprocal_is_correctly_rounded(rt):
-    # div_rn (kernel.hip): x / d from RN(1/d) and Markstein's correction inside the gate, the
-    # compiler's division outside it. The exhaustive significand check is tools/markstein_check.hip
-    # (profiles/r05/markstein_check.log); here random operands over the whole exponent range, the
-    # gate's edges and the special values, against numpy's correctly rounded f32 division.
+def test_cube_side_quotient_from_the_reciprocal_is_the_division(rt):
+    # A BVH cube leaf forms each side's t = (k - o) / d from the ray's reciprocal RN(1/d) and Markstein's
+    # correction when k, o and d are in range (kernel.hip rcp_quotient / rcp_ray_ok), the division
+    # otherwise. The exhaustive significand check is tools/markstein_check.hip
+    # (profiles/r05/markstein_check.log); here random in-range operands over the whole gate, its edges
+    # and the special values, against numpy's correctly rounded f32 arithmetic, bit for bit.
     rng = np.random.default_rng(11)
     n = 1 << 20
-    bits = rng.integers(0, 1 << 32, size=(n, 2), dtype=np.uint64).astype(np.uint32)
-    cases = [bits.view(np.float32)]
-    mant = rng.integers(0, 1 << 23, size=(n, 2), dtype=np.uint32)
-    expo = rng.integers(127 - 70, 127 + 70, size=(n, 2), dtype=np.uint32)
-    cases.append(((expo << 23) | mant).view(np.float32) * np.where(rng.random((n, 2)) < 0.5, -1, 1).astype(np.float32))
-    edge = np.array([0.0, -0.0, 2.0 ** -60, -(2.0 ** -60), 2.0 ** 60, 2.0 ** -61, 2.0 ** 61, 1e-45, 1e-40, 3e38,
-                     np.inf, -np.inf, np.nan, 1.0, -1.0, 3.0, 0.1, 555.0], dtype=np.float32)
-    cases.append(np.array(np.meshgrid(edge, edge)).reshape(2, -1).T.astype(np.float32))
-    a = np.concatenate(cases)
+
+    def ranged(size, lo=-20, hi=20):
+        e = rng.integers(127 + lo, 127 + hi, size=size, dtype=np.uint32)
+        m = rng.integers(0, 1 << 23, size=size, dtype=np.uint32)
+        v = ((e << 23) | m).view(np.float32)
+        return v * np.where(rng.random(size) < 0.5, -1, 1).astype(np.float32)
+
+    cases = [np.stack([ranged(n), ranged(n), ranged(n)], axis=1)]
+    # near-equal k and o (cancellation), zeros, and operands just outside the gate
+    k = ranged(n)
+    o = (k.astype(np.float64) * (1 + rng.normal(0, 1e-6, n))).astype(np.float32)
+    cases.append(np.stack([k, o, ranged(n)], axis=1))
+    edge = np.array([0.0, -0.0, 2.0 ** -20, -(2.0 ** -20), 2.0 ** 20, 2.0 ** -21, 2.0 ** 21, 1e-45, 3e38, np.inf,
+                     np.nan, 1.0, -1.0, 3.0, 0.1, 555.0, 1e-7], dtype=np.float32)
+    g = np.array(np.meshgrid(edge, edge, edge)).reshape(3, -1).T
+    cases.append(g.astype(np.float32))
+    a = np.concatenate(cases).astype(np.float32)
     out = rt.device_kat(4, a)
     with np.errstate(all="ignore"):
-        want = (a[:, 0] / a[:, 1]).astype(np.float32)
-    # the device's own division and div_rn against the host, bit for bit (NaN payloads aside)
-    for col in (1, 0):
+        want = ((a[:, 0] - a[:, 1]) / a[:, 2]).astype(np.float32)
+    for col in (1, 0):  # the device's own division, then the reciprocal form, against the host
         got = out[:, col]
         same = (got.view(np.uint32) == want.view(np.uint32)) | (np.isnan(got) & np.isnan(want))
         assert same.all(), (col, a[~same][:5], got[~same][:5], want[~same][:5])

@@ -6,11 +6,13 @@
 # bench line per config plus a driver-style C3 line, 4. the GPU suite and smoke(). Every GPU step
 # has its own time limit; the script stops at the first failure. gpurun allows 20 minutes per call,
 # so the session runs in two calls: `bash tools/final_evidence.sh profiles` (1-2), then
-# `bash tools/final_evidence.sh bench` (3-4); no argument runs both.
+# `bash tools/final_evidence.sh bench` (3-4); no argument runs both. ROUND (default r05) names the
+# profiles/<ROUND> directory the summaries go to.
 set -u
 PHASE="${1:-all}"
+ROUND="${ROUND:-r05}"
 cd "$(dirname "$0")/.."
-OUT=gpurun_out/final4
+OUT=gpurun_out/final_$ROUND
 mkdir -p "$OUT/pmc"
 export TMPDIR=/tmp
 run() {  # run <log> <seconds> <cmd...>
@@ -27,9 +29,9 @@ run() {  # run <log> <seconds> <cmd...>
 }
 if [ "$PHASE" != bench ]; then
     for c in C3 C1 C2 C4 C5; do
-        run "profile_$c.log" 900 bash tools/profile.sh final4 "$c"
-        run "roofline_$c.log" 120 python3 tools/valu_roofline.py "gpurun_out/prof_final4_$c" --out-dir profiles/r04
-        cp "profiles/r04/pmc_valu_$c.json" "profiles/r04/pmc_traffic_$c.json" "$OUT/pmc/"
+        run "profile_$c.log" 900 bash tools/profile.sh "final_$ROUND" "$c"
+        run "roofline_$c.log" 120 python3 tools/valu_roofline.py "gpurun_out/prof_final_${ROUND}_$c" --out-dir "profiles/$ROUND"
+        cp "profiles/$ROUND/pmc_valu_$c.json" "profiles/$ROUND/pmc_traffic_$c.json" "$OUT/pmc/"
     done
 fi
 if [ "$PHASE" != profiles ]; then
