@@ -11,6 +11,7 @@
 set -u
 PHASE="${1:-all}"
 ROUND="${ROUND:-r05}"
+CFGS="${CFGS:-C3 C1 C2 C4 C5}"  # the configs of this call (a call is limited to ~20 minutes)
 cd "$(dirname "$0")/.."
 OUT=gpurun_out/final_$ROUND
 mkdir -p "$OUT/pmc"
@@ -28,14 +29,14 @@ run() {  # run <log> <seconds> <cmd...>
     fi
 }
 if [ "$PHASE" != bench ]; then
-    for c in C3 C1 C2 C4 C5; do
+    for c in $CFGS; do
         run "profile_$c.log" 900 bash tools/profile.sh "final_$ROUND" "$c"
         run "roofline_$c.log" 120 python3 tools/valu_roofline.py "gpurun_out/prof_final_${ROUND}_$c" --out-dir "profiles/$ROUND"
         cp "profiles/$ROUND/pmc_valu_$c.json" "profiles/$ROUND/pmc_traffic_$c.json" "$OUT/pmc/"
     done
 fi
 if [ "$PHASE" != profiles ]; then
-    for c in C3 C1 C2 C4 C5; do
+    for c in $CFGS; do
         run "bench_$c.log" 300 python3 -u bench.py --config "$c"
     done
     run bench_driver_style.log 300 python3 -u bench.py --gpus 1 --steps 20 --warmup 5
