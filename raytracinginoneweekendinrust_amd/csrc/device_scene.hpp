@@ -162,6 +162,10 @@ struct DevScene {
     // Every rect / cube-side coordinate is +0 or of magnitude in [2^-20, 2^20] (set at upload): a
     // cube leaf's side quotients may then come from the ray's reciprocals (kernel.hip div_rn_safe).
     uint32_t rect_rcp_ok;
+    // The first top-level ConstantMedium when its boundary is one sphere and every entry before it
+    // is a sphere / moving sphere / rect / cube / sphere run or a prunable, translated-only BVH
+    // (kernel.hip medium_first_estimate); ~0 otherwise.
+    uint32_t mb_entry;
 };
 
 // Camera::new (camera.rs:44-81) evaluated on the host.

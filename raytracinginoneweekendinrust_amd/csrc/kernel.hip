@@ -1644,11 +1644,60 @@ RT_DEV bool entry_geom_hit(const DevScene& S, float delta, const DevEntry* E, Ra
     return leaf_hit<kF | kFLeafRM>(S, uni<kF>(E->payload), r, q, tmin, closest, hit_code);  // top level: any primitive
 }
 
+// Medium-first bound (world_hit, fast kernel; DESIGN.md §4 "medium-first bound"). The first
+// top-level ConstantMedium (S.mb_entry, sphere boundary) draws its ln(U) from the stream state the
+// walk starts with, since no entry before it draws. Its scatter point is estimated here in f32 from
+// a peeked draw; world_hit walks the entries before it with t_max = B (a little beyond the estimate
+// C) instead of inf. Any hit <= C of those entries is then found with the same record (a box the
+// reference test rejects at B holds no candidate <= C: the exact-pruning margin of bvh_hit), and if
+// none is found the medium, entered with t_max = inf, scatters where the reference's would with any
+// closest_so_far >= C — which medium_hit checks on the exact values (vbound), handing the sample to
+// the reference kernel otherwise. kInf: no bound (no such medium, the ray misses its sphere or
+// leaves it unscattered by the estimate).
+#ifndef RT_MEDIUM_FIRST
+#define RT_MEDIUM_FIRST 1
+#endif
+#ifndef RT_MB_LANES
+#define RT_MB_LANES 64  // bound only waves with at most this many active lanes
+#endif
+// Compiled into the sphere-BVH preset with marble textures (the book-2 final scene's, C3): same box,
+// same bits, C3 93.4 -> 88.9 ms per 100-spp frame and one rank of 8 60.1 -> 57.2 ms; the BVH-only
+// preset (C1, whose scenes have no media) does without its registers
+// (profiles/r05/experiments/medium_first_ab.log).
+template <uint32_t kF>
+constexpr bool kMediumFirst = RT_MEDIUM_FIRST && (kF & kFBvh) != 0u && (kF & kFMarble) != 0u && (kF & kFTri) == 0u;
+template <uint32_t kF>
+RT_DEV float medium_first_estimate(const DevScene& S, const DevEntry* E, Ray r, const Rng& g, const Key& k) {
+    const uint32_t ntf = E->ntf;
+    for (uint32_t i = 0; i < ntf; ++i) r = apply_op_u<kF>(E->tf[i], r);
+    const DevEntry* B = S.entries + E->payload;
+    Ray rb = r;
+    const uint32_t bn = B->ntf;
+    for (uint32_t i = 0; i < bn; ++i) rb = apply_op_u<kF>(B->tf[i], rb);
+    const f4 s = ld4(S.sph + rtdev::leaf_index(B->payload));
+    const V oc = rb.o - xyz(s);
+    const float a = dot(rb.d, rb.d), hb = dot(oc, rb.d), cq = dot(oc, oc) - s.w * s.w;
+    const float disc = hb * hb - a * cq;
+    if (!(disc >= 0.0f)) return kInf;
+    const float sq = __builtin_sqrtf(disc);
+    const float r2 = (sq - hb) / a;
+    float t1 = (-hb - sq) / a;
+    if (t1 < 0.001f) t1 = 0.001f;
+    if (!(t1 < r2)) return kInf;
+    const float len = length(r.d);
+    Rng p = g;  // the draw medium_hit will make, not consumed here
+    const float hd = E->neg_inv_density * __logf(std01(p, k));
+    if (!(hd < (r2 - t1) * len * (1.0f - 0x1p-10f))) return kInf;  // leaves (or about to): no bound
+    return (t1 + hd / len) * (1.0f + 0x1p-8f) + 0x1p-16f;
+}
+
 // ConstantMedium::hit (hittable.rs:176-233); draws one U(0,1) once the clamped
-// interval is non-empty, exactly where the reference does.
+// interval is non-empty, exactly where the reference does. vbound < inf: world_hit's medium-first
+// bound C (above) with t_max = inf here; the hit must be the one every closest_so_far >= C gives.
 template <int kKind, uint32_t kF>
 RT_DEV bool medium_hit(const DevScene& S, float delta, const DevEntry* E, Ray r, float tmin, float tmax, Rng& g,
-                       const Key& k, float& t_out, uint32_t* stk, uint32_t mode, bool& replay) {
+                       const Key& k, float& t_out, uint32_t* stk, uint32_t mode, bool& replay,
+                       float vbound = kInf) {
     uint32_t ntf = uni<kF>(E->ntf);
     for (uint32_t i = 0; i < ntf; ++i) r = apply_op_u<kF>(E->tf[i], r);
     const DevEntry* B = S.entries + uni<kF>(E->payload);
@@ -1726,6 +1775,12 @@ RT_DEV bool medium_hit(const DevScene& S, float delta, const DevEntry* E, Ray r,
     PROF_T0(pl);
     float hit_distance = E->neg_inv_density * rt_logf(std01(g, k));
     PROF_ADD(kPrLog, pl);
+    if constexpr (kKind == 0 && kMediumFirst<kF>) {
+        if (vbound < kInf) {  // t2 and the inside distance only grow with closest_so_far (monotone roundings)
+            const float t2v = t2 > vbound ? vbound : t2;
+            if (!(t1 < t2v) || hit_distance > (t2v - t1) * ray_length) replay = true;
+        }
+    }
     if (hit_distance > distance_inside) return false;
     t_out = t1 + hit_distance / ray_length;
     return true;
@@ -2161,13 +2216,34 @@ template <int kKind, uint32_t kF>
 RT_DEV bool world_hit(const DevScene& S, float delta, const Ray& r, Rng& g, const Key& k, float& t_hit,
                       uint32_t& hit_entry, uint32_t& hit_code, uint32_t* stk, uint32_t mode, bool& replay) {
     float closest = kInf;
+    float cb = kInf;  // the medium-first bound C (medium_first_estimate)
+    if constexpr (kKind == 0 && kMediumFirst<kF>) {
+        if (S.mb_entry < S.num_top && __builtin_popcountll(__builtin_amdgcn_read_exec()) <= RT_MB_LANES) {
+            cb = medium_first_estimate<kF>(S, S.entries + S.mb_entry, r, g, k);
+            // B = C(1 + 2^-18) + 2 delta / min|d_a|: bvh_hit's inflated-entry margin te - delta * max|inv_a|
+            // (the BVHs before the medium are translated only, so the ray's inverse direction is
+            // theirs; the factor 2 and the 2^-18 cover the roundings of inv and of B itself)
+            const float md = fminf(fabsf(r.d.x), fminf(fabsf(r.d.y), fabsf(r.d.z)));
+            const float b = cb * (1.0f + 0x1p-18f) + (delta + delta) / md;
+            if (b < kInf) closest = b; else cb = kInf;
+        }
+    }
     bool any = false;
     for (uint32_t e = 0; e < S.num_top; ++e) {
         const DevEntry* E = S.entries + e;
         PROF_T0(pe);
         if (uni<kF>(E->kind) == rtdev::kEntMedium) {
-            float t;
-            if (medium_hit<kKind, kF>(S, delta, E, r, 0.001f, closest, g, k, t, stk, mode, replay)) {
+            float t, vb = kInf;
+            if constexpr (kKind == 0 && kMediumFirst<kF>) {
+                if (e == S.mb_entry && closest > cb) {  // nothing <= C before the medium: enter it with inf
+                    closest = kInf;
+                    any = false;
+                    vb = cb;
+                }
+            }
+            const bool mh = medium_hit<kKind, kF>(S, delta, E, r, 0.001f, closest, g, k, t, stk, mode, replay, vb);
+            if (vb < kInf && !mh) replay = true;  // the estimate's scatter point did not hold
+            if (mh) {
                 closest = t;
                 hit_entry = e;
                 hit_code = rtdev::leaf_code(rtdev::kLeafMedium, 0);
@@ -3219,6 +3295,24 @@ int rt_scene_upload(const rt_scene_desc* desc, int device, rt_scene_handle* out)
             const float a = std::fabs(c);
             if (!(b == 0u || (a >= 0x1p-20f && a <= 0x1p20f))) d.rect_rcp_ok = 0u;
         }
+    }
+    d.mb_entry = ~0u;  // the medium-first bound's entry (medium_first_estimate)
+    for (uint32_t e = 0; e < hs.num_top; ++e) {
+        const rtdev::DevEntry& E = hs.entries[e];
+        if (E.kind == rtdev::kEntMedium) {
+            const rtdev::DevEntry& B = hs.entries[E.payload];
+            if (B.kind == rtdev::kEntGeom && rtdev::leaf_type(B.payload) == rtdev::kLeafSphere) d.mb_entry = e;
+            break;
+        }
+        bool ok = E.kind == rtdev::kEntSphereRun;
+        if (E.kind == rtdev::kEntGeom) ok = rtdev::leaf_type(E.payload) != rtdev::kLeafTri;
+        if (E.kind == rtdev::kEntBvh) {
+            uint32_t flag;
+            memcpy(&flag, &hs.nodes[(size_t)E.payload * rtdev::kBvhNodeF4 + 7].w, 4);
+            ok = (flag & rtdev::kBvhPrunable) != 0u;
+            for (uint32_t i = 0; i < E.ntf && i < (uint32_t)rtdev::kMaxTransforms; ++i) ok = ok && E.tf[i].w == 0.0f;
+        }
+        if (!ok) break;
     }
     s->features = (hs.tri.empty() ? 0u : kFTri) | (hs.bvh_rect_msph ? kFLeafRM : 0u);
     for (const rtdev::DevTexture& t : hs.texs)
