@@ -2193,11 +2193,16 @@ RT_DEV void start_sample(const DevCamera& C, const DevParams& P, const Key& k, u
 // 915 (250 spp, or one rank of two) -> 8: 264, 12: 270, 16: 278; 458 (rank of four) -> 4: 138,
 // 8: 144; 366 (100 spp) -> 4: 112, 8: 119; 230 (63 spp, or one rank of eight) -> 2: 77, 4: 74,
 // 8: 82, 16: 97. The fixed 16 cost an 8-GPU rank a third of its time.
+// Round 5 (same box, 500-spp C3 shards, tools/shard_time.py, RT_GROUP sweep): the batches in flight
+// (waves x group units, block-major) span group / (units per wave) of the shard's blocks, and a
+// shard's blocks span the whole image; a rank slows down steeply once that window passes ~4% of
+// the image (one rank of 8, 261 units per wave: group 4 57.1 ms, 8 55.5, 10 55.4, 12 60.1, 16 68.6;
+// of 16: 4 30.9, 6 32.3, 8 36.3) and gains a little from larger batches below it (rank of 4:
+// 8 107.9, 16 106.5; one GPU: 16 415.3, 24 413.1). The flat and triangle presets gain more
+// (one GPU: C5 946 -> 905 ms with 64, C4 1461 -> 1449). So: a 1/32 window, 4..64 units.
 static inline uint32_t batch_group(uint64_t units, uint32_t waves) {
-    const uint64_t per = units / ((uint64_t)(waves ? waves : 1u) * 64u);
-    uint32_t g = 4u;
-    while (g < 16u && 2u * g <= per) g *= 2u;
-    return g;
+    const uint64_t g = units / ((uint64_t)(waves ? waves : 1u) * 32u);
+    return g < 4u ? 4u : g > 64u ? 64u : (uint32_t)g;
 }
 constexpr uint32_t kPermLdsMax = 4u * 9u * 256u;  // up to four Marble textures staged in LDS
 struct ChunkParams {
@@ -2512,6 +2517,17 @@ RT_DEV bool take_sample(ItemPool& pool, bool want, const DevCamera& C, const Dev
                 }
                 if (pool.batch + (item >> 6) >= Q.units) s = Q.samples;  // past the last unit: no work
                 if (!(P.tune & kModeBlocksForward)) blk_local = Q.blocks - 1u - blk_local;
+#ifdef RT_EXP_STRIDE
+                if (P.tune & (1u << 23)) {  // A/B only: blocks in 8 interleave classes, one after another
+                    uint32_t i = blk_local, r = 0u;
+                    for (; r < 7u; ++r) {
+                        const uint32_t cr = (Q.blocks - r + 7u) / 8u;
+                        if (i < cr) break;
+                        i -= cr;
+                    }
+                    blk_local = r + 8u * i;
+                }
+#endif
                 uint32_t pib = item & 63u;
                 sl = blk_local * 64u + pib;
                 uint32_t blk = P.shard_index + blk_local * P.shard_count;

@@ -2,8 +2,9 @@
 
 librtamd_rngdiv.so is kernel.hip with the per-lane branch around the out-of-line Philox call
 (RT_RNG_UNIFORM=0); tools/exec_join_check.py finds the Rng buffer's two split copies ahead of
-that join's EXEC restore in its C1 and C4 instances. Here the fixture renders one sample index
-of C1: the camera segment (depth 1) still matches the oracle, the full path does not, first at
+that join's EXEC restore (in round 4 in its C1 and C4 instances; since round 5's DevScene grew by
+a word, in the all-features instance, which the second case renders). Here the fixture renders
+one sample index of C1: the camera segment (depth 1) still matches the oracle, the full path does not, first at
 pixel (3, 0), whose lane entered its first scatter with r0 = d (tools/trace_sample.py recorded
 r0 = 6, r2 = a stale float, d = 7 on this box). The product renders the same sample bit-exact.
 """
@@ -28,10 +29,15 @@ def test_fixture_leaves_the_oracle_after_the_camera_segment_only(rt, orc):
     from kernel_resources import readable
     fixture = os.path.join(LIB, "librtamd_rngdiv.so")
     assert os.path.exists(fixture), "make -C raytracinginoneweekendinrust_amd/csrc rngdiv"
-    # the fixture reproduces the miscompile only while this compiler still splits the C1
-    # instance's join that way (tests/test_exec_join.py reports it); nothing to render otherwise
-    if not any(readable(fn) == "trace_samples<0, 3, 1>" for fn, _, _ in exec_join_check.check_library(fixture)):
-        pytest.skip("the live fixture's C1 instance has no split copies with this compiler")
+    # the fixture reproduces the miscompile only where this compiler splits the join that way
+    # (tests/test_exec_join.py reports it): the C1 instance, else the all-features instance (its
+    # scene below); nothing to render when neither is split
+    split = {readable(fn) for fn, _, _ in exec_join_check.check_library(fixture)}
+    if "trace_samples<0, 3, 1>" not in split:
+        if not split & {"trace_samples<0, 3, 63>", "trace_samples<0, 4, 63>"}:
+            pytest.skip("the live fixture has no split copies in the C1 or all-features instances")
+        _all_features_fixture(rt, orc, bind(_capi.LIB_PATH, 0), bind(fixture, 1), _capi)
+        return
     cfg = rt.CONFIGS["C1"]
     prod, fix = bind(_capi.LIB_PATH, 0), bind(fixture, 1)
     scene = rt.Scene.generate(cfg.scene, cfg.scene_seed)
@@ -51,3 +57,44 @@ def test_fixture_leaves_the_oracle_after_the_camera_segment_only(rt, orc):
     # a few percent of the frame's samples (those whose lane skipped the draw's block fetch
     # while another lane made it), not a wholesale failure
     assert 0.005 < bad.mean() < 0.2, bad.mean()
+
+
+def _all_features_fixture(rt, orc, prod, fix, _capi):
+    """The same check on the all-features instance: test_gpu_parity's every-preset scene (a long
+    sphere run, a BVH and a triangle), rendered through each library's own C ABI."""
+    import ctypes as C
+    b = rt.SceneBuilder()
+    white = b.lambertian_from_color((0.7, 0.7, 0.7))
+    metal = b.metal((0.8, 0.6, 0.2), 0.1)
+    w = rt.HittableList()
+    for i in range(11):
+        w.add(b.sphere((i - 5.0, 0.3 * (i % 3), -1.0 - 0.2 * (i % 2)), 0.45, metal if i % 2 else white))
+    inner = rt.HittableList()
+    for i in range(12):
+        inner.add(b.sphere((i - 6.0, 1.6, 0.5 * (i % 4)), 0.35, white))
+    w.add(b.bvh(inner, 0.0, 1.0, axis_seed=5))
+    w.add(b.tri((-6, -1, -3), (6, -1, -3), (0, 4, -3), white))
+    w.add(b.sphere((0, -1000.5, 0), 1000.0, white))
+    sc = b.finish(w)
+    cam = rt.Camera.new((0, 2, 9), (0, 0.5, 0), (0, 1, 0), 45.0, 1.5, 0.05, 9.0, 0.0, 0.0)
+
+    def render(lib, depth):
+        h = C.c_void_p()
+        assert lib.rt_scene_upload(sc.desc, 0, C.byref(h)) == 0
+        p = rt.render_params(96, 64, 8, depth, background=(0.6, 0.7, 0.9))
+        img = np.zeros(96 * 64 * 3, dtype=np.float32)
+        st = _capi.rt_stats()
+        d = cam.desc()
+        assert lib.rt_render(h, C.byref(d), C.byref(p), img.ctypes.data_as(C.POINTER(C.c_float)), C.byref(st)) == 0
+        lib.rt_scene_free(h)
+        return img
+
+    def oracle(depth):
+        return np.asarray(orc.render(sc, cam, rt.render_params(96, 64, 8, depth, background=(0.6, 0.7, 0.9)))[0]).ravel()
+
+    want1, want = oracle(1), oracle(12)
+    np.testing.assert_array_equal(render(prod, 12), want)
+    np.testing.assert_array_equal(render(fix, 1), want1)
+    got = render(fix, 12)
+    same = (got == want) | (np.isnan(got) & np.isnan(want))
+    assert not same.all(), "the split copies left every lane's Rng buffer intact"
