@@ -177,9 +177,9 @@ def main() -> int:
     ap.add_argument("--gather", choices=["auto", "ipc", "shm"], default="auto",
                     help="N>1 frame gather transport (frame_gather.FrameGather)")
     ap.add_argument("--pipeline", choices=["auto", "on", "off"], default="auto",
-                    help="two frames in flight per rank (two scene handles and streams): frame k+1's trace "
-                         "kernel takes the SIMDs frame k's last paths leave, and frame k is gathered while "
-                         "frame k+1 renders; auto = on for N>1 (strong scaling), off for one GPU")
+                    help="frames in flight per rank (three scene handles and streams, RT_FLAG_FRAMES_IN_FLIGHT): "
+                         "frame k+1's trace kernel takes the SIMDs frame k's last paths leave, and frame k is "
+                         "gathered while frame k+1 renders; auto = on for N>1 (strong scaling), off for one GPU")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -211,7 +211,12 @@ def main() -> int:
     W, H, spp = cfg.width, cfg.height, cfg.spp
     params, pixels_rank = rank_work(rt, cfg, rank, world, args.scaling, args.exact_bvh)
     pipeline = args.pipeline == "on" or (args.pipeline == "auto" and world > 1)
-    nbuf = 2 if pipeline else 1
+    # Three handles: a handle's launch waits for its previous one, whose replay and resolve kernels get
+    # SIMDs only in the next launch's drain. One rank of 8 on C3: serial 55.9 ms, two handles 55.3, three
+    # with the flag 54.6 (profiles/r05/shard/c3_rank_of_8_frames_in_flight.log).
+    nbuf = 3 if pipeline else 1
+    if pipeline:
+        params.flags |= rt._capi.RT_FLAG_FRAMES_IN_FLIGHT
     # one scene handle per frame in flight (each serialises its own launches and owns its sample buffer)
     dss = [rt.DeviceScene(scene, device=local_rank) for _ in range(nbuf)]
     outs = [torch.zeros(W * H * 3, dtype=torch.float32, device="cuda") for _ in range(nbuf)]
@@ -370,9 +375,10 @@ def main() -> int:
                                             "rt_shard_pull_unpack, or the /dev/shm bounce; no collective)" if world > 1
                                        else "one GPU: the whole frame"),
                        "gather": gather.transport if gather is not None else None,
-                       "pipeline": ("two frames in flight per rank: frame k+1 renders on a second scene handle and "
-                                    "stream while frame k drains and is gathered; every frame is complete and "
-                                    "gathered inside the timed region" if pipeline else None),
+                       "pipeline": ("frames in flight per rank: frame k+1 renders on the next of three scene "
+                                    "handles and streams while frame k drains and is gathered "
+                                    "(RT_FLAG_FRAMES_IN_FLIGHT); every frame is complete and gathered inside the "
+                                    "timed region" if pipeline else None),
                        "exact_bvh": args.exact_bvh},
             "rays_per_s": seg_total / wall_max,
             "segments": int(seg_total),

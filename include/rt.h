@@ -174,6 +174,12 @@ typedef struct rt_camera {
                                  the output instead of starting from zero      */
 #define RT_FLAG_RAW_SUM 8u    /* leave the running sum in the output (no final
                                  division): every slice but the last           */
+#define RT_FLAG_FRAMES_IN_FLIGHT 16u /* the caller overlaps this launch with launches on
+                                 other scene handles of the same device: the
+                                 streaming replay pass, whose waves would start
+                                 in the other launch's drain and leave at once,
+                                 is not launched; the serialized pass re-traces
+                                 every handed-over sample (same bits)          */
 
 typedef struct rt_render_params {
     uint32_t width, height;      /* image size (Renderer::from_aspect_ratio)        */

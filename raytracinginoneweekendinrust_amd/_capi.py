@@ -26,6 +26,7 @@ RT_FLAG_EXACT_BVH = 1
 RT_FLAG_HRPP = 2
 RT_FLAG_ACCUMULATE = 4
 RT_FLAG_RAW_SUM = 8
+RT_FLAG_FRAMES_IN_FLIGHT = 16
 
 # rt_option (rt_set_option): the library's diagnostic switches; it reads no environment
 OPTIONS = {"tune": 0, "group": 1, "stack_lds": 2, "sample_buffer_mb": 3, "hrpp_slot_bits": 4, "launch_log": 5,

@@ -3778,7 +3778,9 @@ int rt_render_launch_camera(rt_scene_handle s, const rt_camera* camera, const rt
             // fast kernel's, free by then (so that launch keeps to the fast kernel's grid).
             const bool deep = (s->features & kFDeep) != 0u;
             const bool kind3 = !(dp.tune & kModeReplayRef);
-            const bool stream_rp = kind3 && !(dp.tune & kModeNoStream);
+            // (not beside launches on other handles, RT_FLAG_FRAMES_IN_FLIGHT: its waves would be
+            // dispatched in the other launch's drain, find this pool full and leave at once)
+            const bool stream_rp = kind3 && !(dp.tune & kModeNoStream) && !(dp.flags & RT_FLAG_FRAMES_IN_FLIGHT);
             if (stream_rp && (e = hipEventRecord(s->fork, st)) != hipSuccess) return hip_fail(e, "replay stream fork");
             hipLaunchKernelGGL(kf, dim3(grid), dim3(64), lds, st, s->dev, cam, dp, q, s->sbuf, s->counter, s->replay,
                                0u, d_segments);

@@ -426,12 +426,12 @@ def test_replay_pass_kernels_match_oracle(cfg_name, w, h, replay_ref, rt, orc):
     assert st["segments"] == cnt["segments"]
 
 
-@pytest.mark.parametrize("stream", [True, False])
+@pytest.mark.parametrize("stream", [True, False, "frames_in_flight"])
 @pytest.mark.parametrize("cfg_name", ["C3", "C5", "C4"])
 def test_streaming_replay_pass_matches_oracle(cfg_name, stream, rt, orc):
     # The streaming replay pass (kernel.hip replay_claim) runs beside the fast kernel and takes
     # the handed-over samples while the fast kernel drains; RT_OPT_TUNE bit 17 leaves them all
-    # to the serialized pass. A 4096 x 1 image (v = j / (H - 1) = NaN: every ray is handed
+    # to the serialized pass, and so does the public RT_FLAG_FRAMES_IN_FLIGHT (bench.py's N > 1 step). A 4096 x 1 image (v = j / (H - 1) = NaN: every ray is handed
     # over) with 8 spp gives 4096 work units, enough to fill the GPU, so the fast kernel's
     # waves drain while the stream's waves wait for slots, and every sample is replayed.
     # C4 is the deep-stack case: its replay runs trace_samples<3, 3, kFAll> and the streaming
@@ -443,7 +443,9 @@ def test_streaming_replay_pass_matches_oracle(cfg_name, stream, rt, orc):
                         cfg.time0, cfg.time1)
     params = rt.render_params(w, h, spp, cfg.depth, background=cfg.background(), seed=9)
     want, cnt = orc.render(scene, cam, params)
-    with rt.options(tune=0 if stream else 1 << 17):
+    if stream == "frames_in_flight":
+        params = rt.render_params(w, h, spp, cfg.depth, background=cfg.background(), seed=9, frames_in_flight=True)
+    with rt.options(tune=1 << 17 if stream is False else 0):
         ds = rt.DeviceScene(scene)
         try:
             for _ in range(2):  # the second render starts from the list the first one freed

@@ -22,8 +22,11 @@ def main():
     ap.add_argument("--spp", type=int, default=None, help="override the config's samples per pixel")
     ap.add_argument("--shard-only", action="store_true", help="skip the whole-frame (1-rank) reference run")
     ap.add_argument("--pipeline", action="store_true",
-                    help="two frames in flight (bench.py --pipeline on): alternate two scene handles and streams "
+                    help="frames in flight (bench.py --pipeline on): rotate scene handles and streams "
                          "and report the steady-state time per step")
+    ap.add_argument("--handles", type=int, default=3, help="scene handles (and streams) in rotation with --pipeline")
+    ap.add_argument("--stream-replay", action="store_true",
+                    help="with --pipeline: keep the streaming replay pass (no RT_FLAG_FRAMES_IN_FLIGHT)")
     a = ap.parse_args()
     import torch
     import raytracinginoneweekendinrust_amd as rt
@@ -37,25 +40,27 @@ def main():
     ds = rt.DeviceScene(scene)
     out = torch.zeros(cfg.width * cfg.height * 3, dtype=torch.float32, device="cuda")
     if a.pipeline:
-        ds2 = rt.DeviceScene(scene)
-        out2 = torch.zeros_like(out)
-        st = [torch.cuda.Stream(), torch.cuda.Stream()]
+        nh = max(2, a.handles)
+        dss = [ds] + [rt.DeviceScene(scene) for _ in range(nh - 1)]
+        outs = [out] + [torch.zeros_like(out) for _ in range(nh - 1)]
+        st = [torch.cuda.Stream() for _ in range(nh)]
         for n in ([a.n] if a.shard_only else sorted({1, a.n})):
             p = rt.render_params(cfg.width, cfg.height, cfg.spp, cfg.depth, background=cfg.background(),
-                                 seed=cfg.render_seed, shard_index=a.rank if n > 1 else 0, shard_count=n)
-            for k in range(2):  # warm-up
-                (ds, ds2)[k % 2].launch(cfg.camera(), p, (out, out2)[k % 2].data_ptr(), 0, st[k % 2].cuda_stream)
+                                 seed=cfg.render_seed, shard_index=a.rank if n > 1 else 0, shard_count=n,
+                                 frames_in_flight=not a.stream_replay)
+            for k in range(nh):  # warm-up
+                dss[k].launch(cfg.camera(), p, outs[k].data_ptr(), 0, st[k].cuda_stream)
             torch.cuda.synchronize()
             import time
             t0 = time.perf_counter()
             for k in range(a.reps):
-                (ds, ds2)[k % 2].launch(cfg.camera(), p, (out, out2)[k % 2].data_ptr(), 0, st[k % 2].cuda_stream)
+                dss[k % nh].launch(cfg.camera(), p, outs[k % nh].data_ptr(), 0, st[k % nh].cuda_stream)
             torch.cuda.synchronize()
             ms = (time.perf_counter() - t0) * 1e3 / a.reps
             print(f"{cfg.name} shard {a.rank if n > 1 else 0}/{n}: pipelined step {ms:.2f} ms "
-                  f"({a.reps} frames, two in flight)", flush=True)
-        ds2.close()
-        ds.close()
+                  f"({a.reps} frames, {nh} handles)", flush=True)
+        for d in dss:
+            d.close()
         return
     for n in ([a.n] if a.shard_only else sorted({1, a.n})):
         p = rt.render_params(cfg.width, cfg.height, cfg.spp, cfg.depth, background=cfg.background(),
