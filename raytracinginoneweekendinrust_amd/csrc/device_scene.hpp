@@ -166,9 +166,6 @@ struct DevScene {
     // is a sphere / moving sphere / rect / cube / sphere run or a prunable, translated-only BVH
     // (kernel.hip medium_first_estimate); ~0 otherwise.
     uint32_t mb_entry;
-    // Entries [gb_first, gb_end): the primitives and sphere runs after the first BVH in the prefix of
-    // the list that precedes any medium and holds only the kinds above (the geometry-first bound).
-    uint32_t gb_first, gb_end;
 };
 
 // Camera::new (camera.rs:44-81) evaluated on the host.

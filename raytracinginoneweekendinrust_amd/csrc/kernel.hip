@@ -1657,9 +1657,6 @@ RT_DEV bool entry_geom_hit(const DevScene& S, float delta, const DevEntry* E, Ra
 #ifndef RT_MEDIUM_FIRST
 #define RT_MEDIUM_FIRST 1
 #endif
-#ifndef RT_GEO_FIRST
-#define RT_GEO_FIRST 0
-#endif
 #ifndef RT_MB_LANES
 #define RT_MB_LANES 64  // bound only waves with at most this many active lanes
 #endif
@@ -2236,27 +2233,6 @@ RT_DEV bool world_hit(const DevScene& S, float delta, const Ray& r, Rng& g, cons
             if (b < kInf) closest = b; else cb = kInf;
         }
     }
-#if RT_GEO_FIRST
-    if constexpr (kKind == 0 && kMediumFirst<kF>) {
-        // Geometry-first bound (EXPERIMENT): the primitives after the first BVH (and before any medium)
-        // tested first; the BVHs before them are then walked with t_max = m(1 + 2^-18) + 2 delta / min|d_a|
-        if (S.gb_first < S.gb_end) {
-            float m = closest;
-            for (uint32_t e = S.gb_first; e < S.gb_end; ++e) {
-                const DevEntry* E = S.entries + e;
-                if (E->kind == rtdev::kEntBvh) continue;
-                uint32_t code;
-                bool rp = false;
-                entry_geom_hit<kKind, kF>(S, delta, E, r, 0.001f, m, code, stk, mode, rp);
-            }
-            if (m < closest) {
-                const float md = fminf(fabsf(r.d.x), fminf(fabsf(r.d.y), fabsf(r.d.z)));
-                const float b = m * (1.0f + 0x1p-18f) + (delta + delta) / md;
-                if (b < closest) closest = b;
-            }
-        }
-    }
-#endif
     bool any = false;
     for (uint32_t e = 0; e < S.num_top; ++e) {
         const DevEntry* E = S.entries + e;
@@ -3337,8 +3313,6 @@ int rt_scene_upload(const rt_scene_desc* desc, int device, rt_scene_handle* out)
         }
     }
     d.mb_entry = ~0u;  // the medium-first bound's entry (medium_first_estimate)
-    d.gb_first = d.gb_end = 0u;  // the geometry-first bound's entries (world_hit)
-    uint32_t first_bvh = ~0u, prefix = 0u;
     for (uint32_t e = 0; e < hs.num_top; ++e) {
         const rtdev::DevEntry& E = hs.entries[e];
         if (E.kind == rtdev::kEntMedium) {
@@ -3346,7 +3320,6 @@ int rt_scene_upload(const rt_scene_desc* desc, int device, rt_scene_handle* out)
             if (B.kind == rtdev::kEntGeom && rtdev::leaf_type(B.payload) == rtdev::kLeafSphere) d.mb_entry = e;
             break;
         }
-        if (E.kind == rtdev::kEntBvh && first_bvh == ~0u) first_bvh = e;
         bool ok = E.kind == rtdev::kEntSphereRun;
         if (E.kind == rtdev::kEntGeom) ok = rtdev::leaf_type(E.payload) != rtdev::kLeafTri;
         if (E.kind == rtdev::kEntBvh) {
@@ -3356,11 +3329,6 @@ int rt_scene_upload(const rt_scene_desc* desc, int device, rt_scene_handle* out)
             for (uint32_t i = 0; i < E.ntf && i < (uint32_t)rtdev::kMaxTransforms; ++i) ok = ok && E.tf[i].w == 0.0f;
         }
         if (!ok) break;
-        prefix = e + 1u;
-    }
-    if (first_bvh < prefix) {
-        d.gb_first = first_bvh + 1u;
-        d.gb_end = prefix;
     }
     s->features = (hs.tri.empty() ? 0u : kFTri) | (hs.bvh_rect_msph ? kFLeafRM : 0u);
     for (const rtdev::DevTexture& t : hs.texs)
