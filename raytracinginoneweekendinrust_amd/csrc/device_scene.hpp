@@ -62,6 +62,7 @@ enum EntryKind : uint32_t {
     kEntMedium = 2,  // payload = boundary entry index; phase_mat, neg_inv_density
     kEntSphereRun = 3,  // payload = first sphere, pad[0] = count: consecutive top-level spheres
                         // (no transforms, consecutive sphere records), tested in list order
+    kEntRectRun = 4,    // payload = first rect, pad[0] = count: the same for rectangles (walls, lights)
 };
 
 constexpr int kMaxTransforms = 3;

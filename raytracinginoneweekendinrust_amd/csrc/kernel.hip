@@ -1604,6 +1604,33 @@ RT_DEV bool entry_geom_hit(const DevScene& S, float delta, const DevEntry* E, Ra
         }
         return any;
     }
+    if (kind == rtdev::kEntRectRun) {  // consecutive untransformed top-level rectangles, in list order
+        const uint32_t first = uni<kF>(E->payload), n = uni<kF>(E->pad[0]);
+        bool any = false;
+        for (uint32_t i = 0; i < n; ++i) {
+            const uint32_t idx = first + i;
+            const f4 r0 = ld4(S.rect + 2 * idx), r1 = ld4(S.rect + 2 * idx + 1);
+            float t;
+            bool h;
+            if constexpr (kUniformEntries<kF>) {  // the plane axis is the wave's (a scalar branch)
+                const uint32_t axis = __builtin_amdgcn_readfirstlane(__float_as_uint(r1.y));
+                if (axis == 0u)  // XY: plane z
+                    h = side_t(r0.x, r.o.z, r.d.z, r.o.x, r.d.x, r.o.y, r.d.y, r0.y, r0.z, r0.w, r1.x, tmin, closest, t);
+                else if (axis == 1u)  // XZ: plane y
+                    h = side_t(r0.x, r.o.y, r.d.y, r.o.x, r.d.x, r.o.z, r.d.z, r0.y, r0.z, r0.w, r1.x, tmin, closest, t);
+                else  // YZ: plane x
+                    h = side_t(r0.x, r.o.x, r.d.x, r.o.y, r.d.y, r.o.z, r.d.z, r0.y, r0.z, r0.w, r1.x, tmin, closest, t);
+            } else {
+                h = rect_t(r0, r1, r, tmin, closest, t);
+            }
+            if (h) {
+                closest = t;
+                hit_code = rtdev::leaf_code(rtdev::kLeafRect, idx);
+                any = true;
+            }
+        }
+        return any;
+    }
     if (kind == rtdev::kEntBvh) {
         if constexpr ((kF & kFBvh) == 0u) {
             return false;  // not reached: the scene has no BVH
@@ -3320,7 +3347,7 @@ int rt_scene_upload(const rt_scene_desc* desc, int device, rt_scene_handle* out)
             if (B.kind == rtdev::kEntGeom && rtdev::leaf_type(B.payload) == rtdev::kLeafSphere) d.mb_entry = e;
             break;
         }
-        bool ok = E.kind == rtdev::kEntSphereRun;
+        bool ok = E.kind == rtdev::kEntSphereRun || E.kind == rtdev::kEntRectRun;
         if (E.kind == rtdev::kEntGeom) ok = rtdev::leaf_type(E.payload) != rtdev::kLeafTri;
         if (E.kind == rtdev::kEntBvh) {
             uint32_t flag;

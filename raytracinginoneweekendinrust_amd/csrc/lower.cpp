@@ -248,8 +248,22 @@ class Lowerer {
         // Consecutive untransformed spheres with consecutive records become one
         // run entry (hittable.rs:100-118 order and closest_so_far unchanged): the
         // device then streams the sphere records without per-entry headers.
+        // Rectangles the same way (kEntRectRun): a Cornell box's walls and light.
         std::vector<rtdev::DevEntry> merged;
         for (const auto& e : top) {
+            const bool rect = e.kind == rtdev::kEntGeom && e.ntf == 0 && rtdev::leaf_type(e.payload) == rtdev::kLeafRect;
+            if (rect && !merged.empty()) {
+                rtdev::DevEntry& b = merged.back();
+                const bool brect = b.kind == rtdev::kEntGeom && b.ntf == 0 && rtdev::leaf_type(b.payload) == rtdev::kLeafRect;
+                const uint32_t bfirst = b.kind == rtdev::kEntRectRun ? b.payload : rtdev::leaf_index(b.payload);
+                const uint32_t bn = b.kind == rtdev::kEntRectRun ? b.pad[0] : 1u;
+                if ((b.kind == rtdev::kEntRectRun || brect) && bfirst + bn == rtdev::leaf_index(e.payload)) {
+                    b.kind = rtdev::kEntRectRun;
+                    b.payload = bfirst;
+                    b.pad[0] = bn + 1u;
+                    continue;
+                }
+            }
             const bool sph = e.kind == rtdev::kEntGeom && e.ntf == 0 &&
                              rtdev::leaf_type(e.payload) == rtdev::kLeafSphere;
             if (sph && !merged.empty()) {
