@@ -252,6 +252,26 @@ RT_DEV float2 ld2_at(const f4* base, uint32_t byte_off) {
     __builtin_memcpy(&v, __builtin_assume_aligned(reinterpret_cast<const char*>(base) + byte_off, 8), sizeof(v));
     return v;
 }
+// Wave-uniform reads of the read-only scene records (top-level entries, their transforms, run and
+// boundary records) through the constant address space: at a uniform address the backend loads
+// them with s_load into SGPRs through the scalar cache, where a global load waits on the vector
+// memory path (two dependent trips per entry: the walls of C4 and C5 took 2,600 wave cycles each).
+#ifndef RT_SCALAR_ENTRIES
+#define RT_SCALAR_ENTRIES 1
+#endif
+#if RT_SCALAR_ENTRIES
+#define RT_AS4 __attribute__((address_space(4)))
+#else
+#define RT_AS4
+#endif
+template <class T>
+RT_DEV const RT_AS4 T* cst(const T* p) {
+    return (const RT_AS4 T*)p;
+}
+RT_DEV f4 ld4c(const f4* p) {
+    const RT_AS4 f4* q = cst(p);
+    return f4{q->x, q->y, q->z, q->w};
+}
 
 struct Ray {
     V o, d;
@@ -1565,11 +1585,11 @@ constexpr uint32_t kRunPretestMin = 8u;  // sphere runs at least this long take 
 template <int kKind, uint32_t kF>
 RT_DEV bool entry_geom_hit(const DevScene& S, float delta, const DevEntry* E, Ray r, float tmin, float& closest,
                            uint32_t& hit_code, uint32_t* stk, uint32_t mode, bool& replay) {
-    uint32_t ntf = uni<kF>(E->ntf);
-    for (uint32_t i = 0; i < ntf; ++i) r = apply_op_u<kF>(E->tf[i], r);
-    const uint32_t kind = uni<kF>(E->kind);
+    uint32_t ntf = uni<kF>(cst(E)->ntf);
+    for (uint32_t i = 0; i < ntf; ++i) r = apply_op_u<kF>(ld4c(&E->tf[i]), r);
+    const uint32_t kind = uni<kF>(cst(E)->kind);
     if (kind == rtdev::kEntSphereRun) {  // consecutive top-level spheres, in list order
-        const uint32_t first = uni<kF>(E->payload), n = uni<kF>(E->pad[0]);
+        const uint32_t first = uni<kF>(cst(E)->payload), n = uni<kF>(cst(E)->pad[0]);
         const RayD q = to_d(r);
         const bool pretest = (kF & kFRuns) && n >= kRunPretestMin && !(mode & kModeNoPretest);  // long lists (random_spheres without a BVH): most spheres are misses
         bool any = false;
@@ -1591,7 +1611,7 @@ RT_DEV bool entry_geom_hit(const DevScene& S, float delta, const DevEntry* E, Ra
         if (pretest) {
             const float a = (r.d.x * r.d.x + r.d.y * r.d.y) + r.d.z * r.d.z;
             for (; i + 1u < n; i += 2u) {  // pairs: one packed pretest, then each sphere in order
-                const f4 s0 = ld4(S.sph + first + i), s1 = ld4(S.sph + first + i + 1u);
+                const f4 s0 = ld4c(S.sph + first + i), s1 = ld4c(S.sph + first + i + 1u);
                 bool m0, m1;
                 spheres_surely_missed2(s0, s1, r, a, m0, m1);
                 test(i, s0, m0);
@@ -1599,17 +1619,17 @@ RT_DEV bool entry_geom_hit(const DevScene& S, float delta, const DevEntry* E, Ra
             }
         }
         for (; i < n; ++i) {
-            const f4 sp = ld4(S.sph + first + i);
+            const f4 sp = ld4c(S.sph + first + i);
             test(i, sp, pretest && sphere_surely_missed(sp, r));
         }
         return any;
     }
     if (kind == rtdev::kEntRectRun) {  // consecutive untransformed top-level rectangles, in list order
-        const uint32_t first = uni<kF>(E->payload), n = uni<kF>(E->pad[0]);
+        const uint32_t first = uni<kF>(cst(E)->payload), n = uni<kF>(cst(E)->pad[0]);
         bool any = false;
         for (uint32_t i = 0; i < n; ++i) {
             const uint32_t idx = first + i;
-            const f4 r0 = ld4(S.rect + 2 * idx), r1 = ld4(S.rect + 2 * idx + 1);
+            const f4 r0 = ld4c(S.rect + 2 * idx), r1 = ld4c(S.rect + 2 * idx + 1);
             float t;
             bool h;
             if constexpr (kUniformEntries<kF>) {  // the plane axis is the wave's (a scalar branch)
@@ -1636,19 +1656,19 @@ RT_DEV bool entry_geom_hit(const DevScene& S, float delta, const DevEntry* E, Ra
             return false;  // not reached: the scene has no BVH
         } else {
             ABLATE(kAbBvh2, float c2 = closest; uint32_t h2 = 0u; bool rp = false;
-                   if (bvh_hit<kKind, kF>(S, delta, E->payload, r, tmin, c2, h2, stk, mode, rp) && h2 == 0x7fffffffu)
+                   if (bvh_hit<kKind, kF>(S, delta, cst(E)->payload, r, tmin, c2, h2, stk, mode, rp) && h2 == 0x7fffffffu)
                        closest = -1.0f;);
-            return bvh_hit<kKind, kF>(S, delta, uni<kF>(E->payload), r, tmin, closest, hit_code, stk, mode, replay);
+            return bvh_hit<kKind, kF>(S, delta, uni<kF>(cst(E)->payload), r, tmin, closest, hit_code, stk, mode, replay);
         }
     }
     if constexpr (kUniformEntries<kF>) {
         // A top-level rectangle (walls, lights): its record is the same for the whole wave, so its
         // plane axis is read once (readfirstlane) and the wave branches on it, instead of every lane
         // selecting the six ray components per axis (rect_axes). Same operations as rect_t.
-        const uint32_t code = __builtin_amdgcn_readfirstlane(E->payload);
+        const uint32_t code = __builtin_amdgcn_readfirstlane(cst(E)->payload);
         if (rtdev::leaf_type(code) == rtdev::kLeafRect) {
             const uint32_t idx = rtdev::leaf_index(code);
-            const f4 r0 = ld4(S.rect + 2 * idx), r1 = ld4(S.rect + 2 * idx + 1);
+            const f4 r0 = ld4c(S.rect + 2 * idx), r1 = ld4c(S.rect + 2 * idx + 1);
             const uint32_t axis = __builtin_amdgcn_readfirstlane(__float_as_uint(r1.y));
             float t;
             bool h;
@@ -1667,8 +1687,8 @@ RT_DEV bool entry_geom_hit(const DevScene& S, float delta, const DevEntry* E, Ra
     }
     RayD q = to_d(r);
     ABLATE(kAbGeom2, float c2 = closest; uint32_t h2 = 0u;
-           if (leaf_hit<kF | kFLeafRM>(S, E->payload, r, q, tmin, c2, h2) && h2 == 0x7fffffffu) closest = -1.0f;);
-    return leaf_hit<kF | kFLeafRM>(S, uni<kF>(E->payload), r, q, tmin, closest, hit_code);  // top level: any primitive
+           if (leaf_hit<kF | kFLeafRM>(S, cst(E)->payload, r, q, tmin, c2, h2) && h2 == 0x7fffffffu) closest = -1.0f;);
+    return leaf_hit<kF | kFLeafRM>(S, uni<kF>(cst(E)->payload), r, q, tmin, closest, hit_code);  // top level: any primitive
 }
 
 // Medium-first bound (world_hit, fast kernel; DESIGN.md §4 "medium-first bound"). The first
@@ -1695,13 +1715,13 @@ template <uint32_t kF>
 constexpr bool kMediumFirst = RT_MEDIUM_FIRST && (kF & kFBvh) != 0u && (kF & kFMarble) != 0u && (kF & kFTri) == 0u;
 template <uint32_t kF>
 RT_DEV float medium_first_estimate(const DevScene& S, const DevEntry* E, Ray r, const Rng& g, const Key& k) {
-    const uint32_t ntf = E->ntf;
-    for (uint32_t i = 0; i < ntf; ++i) r = apply_op_u<kF>(E->tf[i], r);
-    const DevEntry* B = S.entries + E->payload;
+    const uint32_t ntf = cst(E)->ntf;
+    for (uint32_t i = 0; i < ntf; ++i) r = apply_op_u<kF>(ld4c(&E->tf[i]), r);
+    const DevEntry* B = S.entries + cst(E)->payload;
     Ray rb = r;
-    const uint32_t bn = B->ntf;
-    for (uint32_t i = 0; i < bn; ++i) rb = apply_op_u<kF>(B->tf[i], rb);
-    const f4 s = ld4(S.sph + rtdev::leaf_index(B->payload));
+    const uint32_t bn = cst(B)->ntf;
+    for (uint32_t i = 0; i < bn; ++i) rb = apply_op_u<kF>(ld4c(&B->tf[i]), rb);
+    const f4 s = ld4c(S.sph + rtdev::leaf_index(cst(B)->payload));
     const V oc = rb.o - xyz(s);
     const float a = dot(rb.d, rb.d), hb = dot(oc, rb.d), cq = dot(oc, oc) - s.w * s.w;
     const float disc = hb * hb - a * cq;
@@ -1713,7 +1733,7 @@ RT_DEV float medium_first_estimate(const DevScene& S, const DevEntry* E, Ray r, 
     if (!(t1 < r2)) return kInf;
     const float len = length(r.d);
     Rng p = g;  // the draw medium_hit will make, not consumed here
-    const float hd = E->neg_inv_density * __logf(std01(p, k));
+    const float hd = cst(E)->neg_inv_density * __logf(std01(p, k));
     if (!(hd < (r2 - t1) * len * (1.0f - 0x1p-10f))) return kInf;  // leaves (or about to): no bound
     return (t1 + hd / len) * (1.0f + 0x1p-8f) + 0x1p-16f;
 }
@@ -1725,19 +1745,19 @@ template <int kKind, uint32_t kF>
 RT_DEV bool medium_hit(const DevScene& S, float delta, const DevEntry* E, Ray r, float tmin, float tmax, Rng& g,
                        const Key& k, float& t_out, uint32_t* stk, uint32_t mode, bool& replay,
                        float vbound = kInf) {
-    uint32_t ntf = uni<kF>(E->ntf);
-    for (uint32_t i = 0; i < ntf; ++i) r = apply_op_u<kF>(E->tf[i], r);
-    const DevEntry* B = S.entries + uni<kF>(E->payload);
+    uint32_t ntf = uni<kF>(cst(E)->ntf);
+    for (uint32_t i = 0; i < ntf; ++i) r = apply_op_u<kF>(ld4c(&E->tf[i]), r);
+    const DevEntry* B = S.entries + uni<kF>(cst(E)->payload);
     float t1 = kInf, t2 = kInf;
-    const uint32_t bkind = uni<kF>(B->kind), bcode = uni<kF>(B->payload);
+    const uint32_t bkind = uni<kF>(cst(B)->kind), bcode = uni<kF>(cst(B)->payload);
     if (bkind == rtdev::kEntGeom && rtdev::leaf_type(bcode) == rtdev::kLeafSphere) {
         // boundary.hit(-inf, inf) then boundary.hit(t1 + 1e-4, inf) on one sphere:
         // the same two roots, selected against two intervals.
         Ray rb = r;
-        uint32_t bn = uni<kF>(B->ntf);
-        for (uint32_t i = 0; i < bn; ++i) rb = apply_op_u<kF>(B->tf[i], rb);
-        Roots R = sphere_roots(ld4(S.sph + rtdev::leaf_index(bcode)), to_d(rb));
-        ABLATE(kAbMedium2, Roots R2 = sphere_roots(ld4(S.sph + rtdev::leaf_index(B->payload)), to_d(rb));
+        uint32_t bn = uni<kF>(cst(B)->ntf);
+        for (uint32_t i = 0; i < bn; ++i) rb = apply_op_u<kF>(ld4c(&B->tf[i]), rb);
+        Roots R = sphere_roots(ld4c(S.sph + rtdev::leaf_index(bcode)), to_d(rb));
+        ABLATE(kAbMedium2, Roots R2 = sphere_roots(ld4(S.sph + rtdev::leaf_index(cst(B)->payload)), to_d(rb));
                if (R2.r1 == -1.0) t1 = -1.0f;);
         if (!sphere_select(R, -kInf, kInf, t1)) return false;
         if (!sphere_select(R, t1 + 0.0001f, kInf, t2)) return false;
@@ -1749,11 +1769,11 @@ RT_DEV bool medium_hit(const DevScene& S, float delta, const DevEntry* E, Ray r,
         // same bits). Left out of the triangle preset, whose scenes have no cube media and
         // whose register allocation the unused code cost 2.7% (C4).
         Ray rb = r;
-        uint32_t bn = uni<kF>(B->ntf);
-        for (uint32_t i = 0; i < bn; ++i) rb = apply_op_u<kF>(B->tf[i], rb);
+        uint32_t bn = uni<kF>(cst(B)->ntf);
+        for (uint32_t i = 0; i < bn; ++i) rb = apply_op_u<kF>(ld4c(&B->tf[i]), rb);
         const uint32_t idx = rtdev::leaf_index(bcode);
-        const f4 s0 = ld4(S.rect + 2 * idx);
-        const float y1 = ld2(S.rect + 2 * idx + 1, 0).x, z1 = ld2(S.rect + 2 * idx + 5, 0).x;
+        const f4 s0 = ld4c(S.rect + 2 * idx);
+        const float y1 = ld4c(S.rect + 2 * idx + 1).x, z1 = ld4c(S.rect + 2 * idx + 5).x;
         const float x0 = s0.y, x1 = s0.z, y0 = s0.w, z0 = s0.x;
         const float ox = rb.o.x, oy = rb.o.y, oz = rb.o.z, dx = rb.d.x, dy = rb.d.y, dz = rb.d.z;
         float tt[6];
@@ -1800,7 +1820,7 @@ RT_DEV bool medium_hit(const DevScene& S, float delta, const DevEntry* E, Ray r,
     float ray_length = length(r.d);
     float distance_inside = (t2 - t1) * ray_length;
     PROF_T0(pl);
-    float hit_distance = E->neg_inv_density * rt_logf(std01(g, k));
+    float hit_distance = cst(E)->neg_inv_density * rt_logf(std01(g, k));
     PROF_ADD(kPrLog, pl);
     if constexpr (kKind == 0 && kMediumFirst<kF>) {
         if (vbound < kInf) {  // t2 and the inside distance only grow with closest_so_far (monotone roundings)
@@ -2264,7 +2284,7 @@ RT_DEV bool world_hit(const DevScene& S, float delta, const Ray& r, Rng& g, cons
     for (uint32_t e = 0; e < S.num_top; ++e) {
         const DevEntry* E = S.entries + e;
         PROF_T0(pe);
-        if (uni<kF>(E->kind) == rtdev::kEntMedium) {
+        if (uni<kF>(cst(E)->kind) == rtdev::kEntMedium) {
             float t, vb = kInf;
             if constexpr (kKind == 0 && kMediumFirst<kF>) {
                 if (e == S.mb_entry && closest > cb) {  // nothing <= C before the medium: enter it with inf
@@ -2318,7 +2338,7 @@ RT_DEV void world_walk(const DevScene& S, float delta, const Ray& ray, Rng& g, c
         if (!(active && w.pos == e)) continue;
         PROF_T0(pe);
         const DevEntry* E = S.entries + e;
-        const uint32_t kind = uni<kF>(E->kind);
+        const uint32_t kind = uni<kF>(cst(E)->kind);
         if (kind == rtdev::kEntMedium) {
             float t;
             if (medium_hit<0, kF>(S, delta, E, ray, 0.001f, w.closest, g, k, t, stk, mode, replay)) {
@@ -2330,9 +2350,9 @@ RT_DEV void world_walk(const DevScene& S, float delta, const Ray& ray, Rng& g, c
             w.pos = e + 1u;
         } else if ((kF & kFBvh) && kind == rtdev::kEntBvh) {
             Ray r = ray;
-            const uint32_t ntf = uni<kF>(E->ntf);
-            for (uint32_t i = 0; i < ntf; ++i) r = apply_op_u<kF>(E->tf[i], r);
-            const uint32_t root = uni<kF>(E->payload);
+            const uint32_t ntf = uni<kF>(cst(E)->ntf);
+            for (uint32_t i = 0; i < ntf; ++i) r = apply_op_u<kF>(ld4c(&E->tf[i]), r);
+            const uint32_t root = uni<kF>(cst(E)->payload);
             const f4* wrapper = S.nodes + (size_t)root * rtdev::kBvhNodeF4;
             const V inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
             if (!w.resume) {  // bvh_hit's hand-over rule (NaN-prone rays go to the reference kernel)
