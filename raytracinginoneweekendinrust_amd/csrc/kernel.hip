@@ -674,13 +674,19 @@ constexpr uint32_t kFSusp = 64u;
 [[maybe_unused]] constexpr uint32_t kStackLdsMax = 19u;  // LDS stack entries per lane at most (9.5 KB per wave: 16 waves/CU)
 // One leaf (primitive or cube). tmax = closest so far; a hit with t == closest is
 // accepted, so later candidates win ties exactly like hittable.rs:110-116.
-template <uint32_t kF = kFAll, bool kInv = false>
+// kTop: a top-level entry's primitive, at a wave-uniform address (ld4c: scalar loads)
+template <bool kC>
+RT_DEV f4 ldt(const f4* p) {
+    if constexpr (kC) return ld4c(p);
+    return ld4(p);
+}
+template <uint32_t kF = kFAll, bool kInv = false, bool kTop = false>
 RT_DEV bool leaf_hit(const DevScene& S, uint32_t code, const Ray& r, const RayD& q, float tmin, float& closest,
                      uint32_t& hit_code, V inv = V{0.0f, 0.0f, 0.0f}) {
     uint32_t type = rtdev::leaf_type(code), idx = rtdev::leaf_index(code);
     float t;
     if (type == rtdev::kLeafSphere) {
-        if (sphere_t(ld4(S.sph + idx), q, tmin, closest, t)) {
+        if (sphere_t(ldt<kTop>(S.sph + idx), q, tmin, closest, t)) {
             closest = t;
             hit_code = code;
             return true;
@@ -688,7 +694,7 @@ RT_DEV bool leaf_hit(const DevScene& S, uint32_t code, const Ray& r, const RayD&
         return false;
     }
     if ((kF & kFLeafRM) && type == rtdev::kLeafRect) {
-        if (rect_t(ld4(S.rect + 2 * idx), ld4(S.rect + 2 * idx + 1), r, tmin, closest, t)) {
+        if (rect_t(ldt<kTop>(S.rect + 2 * idx), ldt<kTop>(S.rect + 2 * idx + 1), r, tmin, closest, t)) {
             closest = t;
             hit_code = code;
             return true;
@@ -699,8 +705,8 @@ RT_DEV bool leaf_hit(const DevScene& S, uint32_t code, const Ray& r, const RayD&
         // The sides' axes are fixed (cube.rs:25-74: xy z0, xy z1, xz y0, xz y1,
         // yz x0, yz x1) and their bounds are the box's six values, read from the
         // records of sides 0 and 2: (z0, x0, x1, y0), y1 and (y0, x0, x1, z0), z1.
-        const f4 s0 = ld4(S.rect + 2 * idx);
-        const float y1 = ld2(S.rect + 2 * idx + 1, 0).x, z1 = ld2(S.rect + 2 * idx + 5, 0).x;
+        const f4 s0 = ldt<kTop>(S.rect + 2 * idx);
+        const float y1 = ldt<kTop>(S.rect + 2 * idx + 1).x, z1 = ldt<kTop>(S.rect + 2 * idx + 5).x;
         const float x0 = s0.y, x1 = s0.z, y0 = s0.w, z0 = s0.x;
         const float ox = r.o.x, oy = r.o.y, oz = r.o.z, dx = r.d.x, dy = r.d.y, dz = r.d.z;
         bool any = false;
@@ -724,7 +730,7 @@ RT_DEV bool leaf_hit(const DevScene& S, uint32_t code, const Ray& r, const RayD&
         return any;
     }
     if ((kF & kFTri) && type == rtdev::kLeafTri) {
-        if (tri_t(ld4(S.tri + 3 * idx), ld4(S.tri + 3 * idx + 1), ld4(S.tri + 3 * idx + 2), r, tmin, closest, t)) {
+        if (tri_t(ldt<kTop>(S.tri + 3 * idx), ldt<kTop>(S.tri + 3 * idx + 1), ldt<kTop>(S.tri + 3 * idx + 2), r, tmin, closest, t)) {
             closest = t;
             hit_code = code;
             return true;
@@ -732,7 +738,7 @@ RT_DEV bool leaf_hit(const DevScene& S, uint32_t code, const Ray& r, const RayD&
         return false;
     }
     if ((kF & kFLeafRM) && type == rtdev::kLeafMSphere) {
-        if (msphere_t(ld4(S.msph + 3 * idx), ld4(S.msph + 3 * idx + 1), ld4(S.msph + 3 * idx + 2), r, tmin, closest,
+        if (msphere_t(ldt<kTop>(S.msph + 3 * idx), ldt<kTop>(S.msph + 3 * idx + 1), ldt<kTop>(S.msph + 3 * idx + 2), r, tmin, closest,
                       t)) {
             closest = t;
             hit_code = code;
@@ -1142,7 +1148,7 @@ RT_DEV void trav_audit(const DevScene& S, const f4* wrapper, uint32_t root, cons
     const bool any = tv.any;
     float c2 = tv.tmax_entry;
     uint32_t h2 = 0u;
-    bool a2 = bvh_hit_reference(S, __float_as_uint(wrapper[7].z), r, to_d(r), inv, tmin, c2, h2, stk);
+    bool a2 = bvh_hit_reference(S, __float_as_uint(ld4c(wrapper + 7).z), r, to_d(r), inv, tmin, c2, h2, stk);
     bool same = a2 == any && (!any || (__float_as_uint(c2) == __float_as_uint(closest) && h2 == hit_code));
     if (!same) {
         unsigned i_ = atomicAdd(&g_trav_audit_count, 1u);
@@ -1178,7 +1184,7 @@ RT_DEV bool bvh_hit(const DevScene& S, float delta, uint32_t root, const Ray& r,
     const V inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
     if constexpr (kKind == 1 || kKind == 2) {
         const RayD q = to_d(r);
-        const uint32_t w2 = __float_as_uint(wrapper[7].z);
+        const uint32_t w2 = __float_as_uint(ld4c(wrapper + 7).z);
         if constexpr (kKind == 2) {
             const uint32_t pid = __float_as_uint(S.nodes2[4 * (size_t)w2 + 3].z);
             if (pid) return bvh_hit_hrpp(S, w2, pid, r, q, inv, tmin, closest, hit_code, stk);
@@ -1200,7 +1206,7 @@ RT_DEV bool bvh_hit(const DevScene& S, float delta, uint32_t root, const Ray& r,
                           __builtin_fabsf(r.o.z) < kInf;
         if constexpr (kKind == 3) {
             if (!fast)
-                return bvh_hit_reference(S, __float_as_uint(wrapper[7].z), r, to_d(r), inv, tmin, closest, hit_code,
+                return bvh_hit_reference(S, __float_as_uint(ld4c(wrapper + 7).z), r, to_d(r), inv, tmin, closest, hit_code,
                                          stk);
         }
         if (!fast) {
@@ -1231,7 +1237,7 @@ template <int kKind, uint32_t kF, bool kSusp>
 RT_DEV bool bvh_run(const DevScene& S, float delta, const f4* wrapper, const Ray& r, V inv, float tmin, float& closest,
                     uint32_t& hit_code, uint32_t* stk, uint32_t mode, Trav& tv, uint32_t susp) {
     const float tmax_entry = tv.tmax_entry;
-    const bool prune = (__float_as_uint(wrapper[7].w) & rtdev::kBvhPrunable) != 0u || (mode & kModePruneAllExp);
+    const bool prune = (__float_as_uint(ld4c(wrapper + 7).w) & rtdev::kBvhPrunable) != 0u || (mode & kModePruneAllExp);
     const float dmi = delta * fmaxf(fmaxf(__builtin_fabsf(inv.x), __builtin_fabsf(inv.y)), __builtin_fabsf(inv.z));
     const bool leaf_boxes = prune && !(mode & kModeNoLeafBoxes);
     // Byte offsets of each axis's near-plane row in a node (min.a rows 0-2, max.a rows 3-5;
@@ -1688,7 +1694,7 @@ RT_DEV bool entry_geom_hit(const DevScene& S, float delta, const DevEntry* E, Ra
     RayD q = to_d(r);
     ABLATE(kAbGeom2, float c2 = closest; uint32_t h2 = 0u;
            if (leaf_hit<kF | kFLeafRM>(S, cst(E)->payload, r, q, tmin, c2, h2) && h2 == 0x7fffffffu) closest = -1.0f;);
-    return leaf_hit<kF | kFLeafRM>(S, uni<kF>(cst(E)->payload), r, q, tmin, closest, hit_code);  // top level: any primitive
+    return leaf_hit<kF | kFLeafRM, false, true>(S, uni<kF>(cst(E)->payload), r, q, tmin, closest, hit_code);  // top level: any primitive
 }
 
 // Medium-first bound (world_hit, fast kernel; DESIGN.md §4 "medium-first bound"). The first
