@@ -167,6 +167,9 @@ struct DevScene {
     // is a sphere / moving sphere / rect / cube / sphere run or a prunable, translated-only BVH
     // (kernel.hip medium_first_estimate); ~0 otherwise.
     uint32_t mb_entry;
+    // Material and texture records (32 B each) of a small scene, in that order; the flat-list
+    // preset's fast kernel stages them in LDS when the launch sets mt_lds (their byte size).
+    uint32_t num_mats, num_texs, mt_lds;
 };
 
 // Camera::new (camera.rs:44-81) evaluated on the host.

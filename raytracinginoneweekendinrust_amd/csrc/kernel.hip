@@ -230,7 +230,7 @@ RT_DEV bool sign_negative_d(double x) { return (__double_as_longlong(x) >> 63) !
 RT_DEV V xyz(f4 a) { return V{a.x, a.y, a.z}; }
 // Scene rows are read through memcpy from their declared alignment, not by punning an f4
 // pointer as float2 / float4 (no type-based aliasing assumption is involved in any load).
-RT_DEV float2 ld2(const f4* p, uint32_t row) {  // the .xy half of row `row`
+[[maybe_unused]] RT_DEV float2 ld2(const f4* p, uint32_t row) {  // the .xy half of row `row` (audit and ablation builds)
     float2 v;
     __builtin_memcpy(&v, __builtin_assume_aligned(p + row, 16), sizeof(v));
     return v;
@@ -2258,6 +2258,10 @@ static inline uint32_t batch_group(uint64_t units, uint32_t waves) {
     return g < 4u ? 4u : g > 64u ? 64u : (uint32_t)g;
 }
 constexpr uint32_t kPermLdsMax = 4u * 9u * 256u;  // up to four Marble textures staged in LDS
+#ifndef RT_MT_LDS
+#define RT_MT_LDS 1
+#endif
+constexpr uint32_t kMtLdsMax = 2048u;  // material + texture records staged in LDS by the flat-list preset
 struct ChunkParams {
     uint32_t sample0;         // global sample index of chunk sample 0 (includes P.sample_base)
     uint32_t samples;         // samples per pixel in this chunk
@@ -2772,6 +2776,22 @@ __global__ __launch_bounds__(64, kWaves) void trace_samples(DevScene Sg, DevCame
         for (uint32_t i = lane; i < S.perm_bytes / 4u; i += 64u) tab[i] = src[i];
         __syncthreads();
         S.perm = reinterpret_cast<const uint8_t*>(tab);
+    }
+    if constexpr (kKind == 0 && (kF & (kFBvh | kFTri | kFMarble)) == 0u) {
+        // The flat-list preset (C5): a small scene's materials and textures behind the stack, so the
+        // per-lane material / texture reads of every shading step hit LDS instead of the vector memory
+        // path (the region profile put C5's emission and texture steps, mostly those loads' waits, at 19%)
+        if (S.mt_lds) {
+            uint32_t* tab = lds_stack + S.stack_depth * 128u;
+            const uint32_t nm = S.num_mats * (sizeof(DevMaterial) / 4u), nt = S.num_texs * (sizeof(DevTexture) / 4u);
+            const uint32_t* sm = reinterpret_cast<const uint32_t*>(Sg.mats);
+            const uint32_t* st = reinterpret_cast<const uint32_t*>(Sg.texs);
+            for (uint32_t i = lane; i < nm; i += 64u) tab[i] = sm[i];
+            for (uint32_t i = lane; i < nt; i += 64u) tab[nm + i] = st[i];
+            __syncthreads();
+            S.mats = reinterpret_cast<const DevMaterial*>(tab);
+            S.texs = reinterpret_cast<const DevTexture*>(tab + nm);
+        }
     }
     if (kKind == 2) {  // HRPP counters behind the stack and the Perlin tables
         const uint32_t perm_words =
@@ -3335,6 +3355,9 @@ int rt_scene_upload(const rt_scene_desc* desc, int device, rt_scene_handle* out)
     d.nodes = (const f4*)(base + parts[6].off);
     d.mats = (const DevMaterial*)(base + parts[7].off);
     d.texs = (const DevTexture*)(base + parts[8].off);
+    d.num_mats = (uint32_t)hs.mats.size();
+    d.num_texs = (uint32_t)hs.texs.size();
+    d.mt_lds = 0u;  // set per launch (the flat-list preset)
     d.perm = base + parts[9].off;
     d.texels = base + parts[10].off;
     d.nodes2 = (const f4*)(base + parts[11].off);
@@ -3728,7 +3751,12 @@ int rt_render_launch_camera(rt_scene_handle s, const rt_camera* camera, const rt
     dev_ref.stack_depth = s->stack_ref;
     const size_t perm_lds =
         s->dev.perm_bytes != 0u && s->dev.perm_bytes <= kPermLdsMax && !(dp.tune & kModeNoPermLds) ? s->dev.perm_bytes : 0u;
-    const size_t lds = (size_t)s->dev.stack_depth * 128u * sizeof(uint32_t) + perm_lds;
+    size_t lds = (size_t)s->dev.stack_depth * 128u * sizeof(uint32_t) + perm_lds;
+    // the flat-list preset stages a small scene's materials and textures behind the stack
+    const size_t mt_bytes = (size_t)(s->dev.num_mats + s->dev.num_texs) * 32u;
+    const bool mt_stage = RT_MT_LDS && s->features == 0u && perm_lds == 0u && mt_bytes <= kMtLdsMax;
+    s->dev.mt_lds = mt_stage ? (uint32_t)mt_bytes : 0u;
+    if (mt_stage) lds += mt_bytes;
     size_t lds_ref = (size_t)dev_ref.stack_depth * 128u * sizeof(uint32_t) + perm_lds;
     if ((dp.flags & RT_FLAG_HRPP) && s->dev.hrpp_npred) {  // the experiment: reference kernel + predictors
         dp.flags |= RT_FLAG_EXACT_BVH;
