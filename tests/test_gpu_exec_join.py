@@ -34,10 +34,20 @@ def test_fixture_leaves_the_oracle_after_the_camera_segment_only(rt, orc):
     # scene below); nothing to render when neither is split
     split = {readable(fn) for fn, _, _ in exec_join_check.check_library(fixture)}
     if "trace_samples<0, 3, 1>" not in split:
-        if not split & {"trace_samples<0, 3, 63>", "trace_samples<0, 4, 63>"}:
-            pytest.skip("the live fixture has no split copies in the C1 or all-features instances")
-        _all_features_fixture(rt, orc, bind(_capi.LIB_PATH, 0), bind(fixture, 1), _capi)
-        return
+        if split & {"trace_samples<0, 3, 63>", "trace_samples<0, 4, 63>"}:
+            _all_features_fixture(rt, orc, bind(_capi.LIB_PATH, 0), bind(fixture, 1), _capi)
+            return
+        # another preset's instance: that config at a reduced width, the fixture forced onto the
+        # split instance's wave count (RT_OPT_TUNE kModeW3 = 0x40 / kModeW4 = 0x400000)
+        presets = {"1": "C1", "33": "C3", "75": "C4", "0": "C5", "4": "C2"}
+        for inst in sorted(split):
+            waves, kf = inst[len("trace_samples<0, "):-1].split(", ")
+            if kf.rstrip("u") in presets:
+                tune = "0x40" if waves == "3" else "0x400000"
+                _config_fixture(rt, orc, presets[kf.rstrip("u")], bind(_capi.LIB_PATH, 0), bind(f"{fixture}:{tune}", 1),
+                                render)
+                return
+        pytest.skip(f"the live fixture's split instances {sorted(split)} have no config here")
     cfg = rt.CONFIGS["C1"]
     prod, fix = bind(_capi.LIB_PATH, 0), bind(fixture, 1)
     scene = rt.Scene.generate(cfg.scene, cfg.scene_seed)
@@ -96,5 +106,27 @@ def _all_features_fixture(rt, orc, prod, fix, _capi):
     np.testing.assert_array_equal(render(prod, 12), want)
     np.testing.assert_array_equal(render(fix, 1), want1)
     got = render(fix, 12)
+    same = (got == want) | (np.isnan(got) & np.isnan(want))
+    assert not same.all(), "the split copies left every lane's Rng buffer intact"
+
+
+def _config_fixture(rt, orc, name, prod, fix, render):
+    """One sample index of config `name` at width 240: the product renders the oracle's image, the
+    fixture renders the camera segment right and leaves the oracle somewhere after it."""
+    cfg = rt.CONFIGS[name]
+    cfg = cfg.scaled(240, 1)
+    from raytracinginoneweekendinrust_amd import _capi
+    scene = rt.Scene.generate(cfg.scene, cfg.scene_seed)
+
+    def oracle(depth):
+        p = rt.render_params(cfg.width, cfg.height, 1, depth, background=cfg.background(), seed=cfg.render_seed,
+                             sample_base=0)
+        img, _ = orc.render(scene, cfg.camera(), p, threads=8)
+        return img.reshape(cfg.height, cfg.width, 3)
+
+    want1, want = oracle(1), oracle(cfg.depth)
+    np.testing.assert_array_equal(render(prod, cfg, rt, _capi, 0)[0], want)
+    np.testing.assert_array_equal(render(fix, cfg, rt, _capi, 0, depth=1)[0], want1)
+    got = render(fix, cfg, rt, _capi, 0)[0]
     same = (got == want) | (np.isnan(got) & np.isnan(want))
     assert not same.all(), "the split copies left every lane's Rng buffer intact"
