@@ -111,8 +111,10 @@ def _all_features_fixture(rt, orc, prod, fix, _capi):
 
 
 def _config_fixture(rt, orc, name, prod, fix, render):
-    """One sample index of config `name` at width 240: the product renders the oracle's image, the
-    fixture renders the camera segment right and leaves the oracle somewhere after it."""
+    """One sample index of config `name` at width 240: the product renders the oracle's image and
+    the fixture does not. (Where the split join sits decides which segment goes wrong first: in
+    C1's instance it came after the camera segment, in C3's 3-wave instance the camera segment
+    itself already differs in 78 of 115,200 values; so only the C1 case checks depth 1.)"""
     cfg = rt.CONFIGS[name]
     cfg = cfg.scaled(240, 1)
     from raytracinginoneweekendinrust_amd import _capi
@@ -124,9 +126,8 @@ def _config_fixture(rt, orc, name, prod, fix, render):
         img, _ = orc.render(scene, cfg.camera(), p, threads=8)
         return img.reshape(cfg.height, cfg.width, 3)
 
-    want1, want = oracle(1), oracle(cfg.depth)
+    want = oracle(cfg.depth)
     np.testing.assert_array_equal(render(prod, cfg, rt, _capi, 0)[0], want)
-    np.testing.assert_array_equal(render(fix, cfg, rt, _capi, 0, depth=1)[0], want1)
     got = render(fix, cfg, rt, _capi, 0)[0]
     same = (got == want) | (np.isnan(got) & np.isnan(want))
     assert not same.all(), "the split copies left every lane's Rng buffer intact"
