@@ -21,6 +21,9 @@ LIB = os.path.join(ROOT, "raytracinginoneweekendinrust_amd", "_lib")
 
 
 def test_fixture_leaves_the_oracle_after_the_camera_segment_only(rt, orc):
+    # (the name is round 4's, when the split sat after C1's camera segment; which segment goes
+    # wrong first depends on where the split join is, so only "the fixture leaves the oracle and
+    # the product does not" is asserted)
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     from ab_time import bind
     from diff_samples import render
@@ -30,43 +33,22 @@ def test_fixture_leaves_the_oracle_after_the_camera_segment_only(rt, orc):
     fixture = os.path.join(LIB, "librtamd_rngdiv.so")
     assert os.path.exists(fixture), "make -C raytracinginoneweekendinrust_amd/csrc rngdiv"
     # the fixture reproduces the miscompile only where this compiler splits the join that way
-    # (tests/test_exec_join.py reports it): the C1 instance, else the all-features instance (its
-    # scene below); nothing to render when neither is split
+    # (tests/test_exec_join.py reports it); render the preset whose instance is split, or skip
     split = {readable(fn) for fn, _, _ in exec_join_check.check_library(fixture)}
-    if "trace_samples<0, 3, 1>" not in split:
-        if split & {"trace_samples<0, 3, 63>", "trace_samples<0, 4, 63>"}:
-            _all_features_fixture(rt, orc, bind(_capi.LIB_PATH, 0), bind(fixture, 1), _capi)
+    if split & {"trace_samples<0, 3, 63>", "trace_samples<0, 4, 63>"}:
+        _all_features_fixture(rt, orc, bind(_capi.LIB_PATH, 0), bind(fixture, 1), _capi)
+        return
+    # a preset's instance: that config at a reduced width, the fixture forced onto the split
+    # instance's wave count (RT_OPT_TUNE kModeW3 = 0x40 / kModeW4 = 0x400000)
+    presets = {"1": "C1", "33": "C3", "75": "C4", "0": "C5", "4": "C2"}
+    for inst in sorted(split):
+        waves, kf = inst[len("trace_samples<0, "):-1].split(", ")
+        if kf.rstrip("u") in presets:
+            tune = "0x40" if waves == "3" else "0x400000"
+            _config_fixture(rt, orc, presets[kf.rstrip("u")], bind(_capi.LIB_PATH, 0), bind(f"{fixture}:{tune}", 1),
+                            render)
             return
-        # another preset's instance: that config at a reduced width, the fixture forced onto the
-        # split instance's wave count (RT_OPT_TUNE kModeW3 = 0x40 / kModeW4 = 0x400000)
-        presets = {"1": "C1", "33": "C3", "75": "C4", "0": "C5", "4": "C2"}
-        for inst in sorted(split):
-            waves, kf = inst[len("trace_samples<0, "):-1].split(", ")
-            if kf.rstrip("u") in presets:
-                tune = "0x40" if waves == "3" else "0x400000"
-                _config_fixture(rt, orc, presets[kf.rstrip("u")], bind(_capi.LIB_PATH, 0), bind(f"{fixture}:{tune}", 1),
-                                render)
-                return
-        pytest.skip(f"the live fixture's split instances {sorted(split)} have no config here")
-    cfg = rt.CONFIGS["C1"]
-    prod, fix = bind(_capi.LIB_PATH, 0), bind(fixture, 1)
-    scene = rt.Scene.generate(cfg.scene, cfg.scene_seed)
-
-    def oracle(depth):
-        p = rt.render_params(cfg.width, cfg.height, 1, depth, background=cfg.background(), seed=cfg.render_seed,
-                             sample_base=0)
-        img, _ = orc.render(scene, cfg.camera(), p, threads=8)
-        return img.reshape(cfg.height, cfg.width, 3)
-
-    want1, want = oracle(1), oracle(cfg.depth)
-    np.testing.assert_array_equal(render(prod, cfg, rt, _capi, 0)[0], want)
-    np.testing.assert_array_equal(render(fix, cfg, rt, _capi, 0, depth=1)[0], want1)
-    got = render(fix, cfg, rt, _capi, 0)[0]
-    bad = (got != want).any(axis=2)
-    assert bad[0, 3], "pixel (3, 0), sample 0: the traced lane"
-    # a few percent of the frame's samples (those whose lane skipped the draw's block fetch
-    # while another lane made it), not a wholesale failure
-    assert 0.005 < bad.mean() < 0.2, bad.mean()
+    pytest.skip(f"the live fixture has no split instance this test can render ({sorted(split)})")
 
 
 def _all_features_fixture(rt, orc, prod, fix, _capi):
