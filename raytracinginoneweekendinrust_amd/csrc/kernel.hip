@@ -3730,12 +3730,14 @@ int rt_render_launch_camera(rt_scene_handle s, const rt_camera* camera, const rt
     }
     // The fast kernel's instance: four waves per SIMD when that raises its occupancy
     // over three (the Perlin tables then stay in L2, so the stack alone sets LDS) — except
-    // for the BVH-only and triangle-BVH presets, whose 4-wave instances spill more than the
-    // extra wave buys (same box, 3 vs 4 waves: C1 4.1 vs 4.4 ms, C4 at 50 spp 112.1 vs
-    // 121.4 ms; the Marble, sphere-run and flat presets stay at 4: C3 +14%, C2 +12%, C5 +10%
-    // at 3; profiles/r02/w3/).
+    // for the BVH-only preset, whose 4-wave instance spills more than the extra wave buys
+    // (same box, 3 vs 4 waves: C1 3.8 vs 4.1 ms; profiles/r05/experiments/waves_3v4_ab.log).
+    // The triangle-BVH preset preferred 3 until round 5 (C4 at 50 spp 112.1 vs 121.4 ms in
+    // round 2); with the rect runs and scalar entry reads its 4-wave instance is 2.2% faster
+    // (1266 -> 1238 ms per frame). The Marble, sphere-run and flat presets stay at 4 (C3 +14%,
+    // C2 +12%, C5 +10% over 3; profiles/r02/w3/).
     const uint32_t preset_feats = s->features & ~kFDeep;
-    const bool prefer3 = preset_feats == kFBvh || preset_feats == (kFBvh | kFTri);
+    const bool prefer3 = preset_feats == kFBvh;
     if (s->fast_waves == 0) {
         const size_t stack_lds = (size_t)s->dev.stack_depth * 128u * sizeof(uint32_t);
         const size_t perm3 = s->dev.perm_bytes != 0u && s->dev.perm_bytes <= kPermLdsMax ? s->dev.perm_bytes : 0u;
