@@ -82,6 +82,8 @@ constexpr uint32_t kModePruneAllExp = 1u << 20;
 constexpr uint32_t kModeBlocksForward = 1u << 21;
 // W4 (RT_OPT_TUNE, A/B only): the 4-wave instance also for the presets that prefer 3 (below).
 constexpr uint32_t kModeW4 = 1u << 22;
+// MbShrink (RT_OPT_TUNE, audit build only): halves the medium-first estimate (world_hit)
+[[maybe_unused]] constexpr uint32_t kModeMbShrink = 1u << 29;
 #ifdef RT_ABLATE
 // Ablation build (librtamd_ablate.so, diagnostics only): RT_OPT_TUNE bits that run a
 // piece of work twice (results of the copy discarded through an opaque test),
@@ -2282,6 +2284,11 @@ RT_DEV bool world_hit(const DevScene& S, float delta, const Ray& r, Rng& g, cons
     if constexpr (kKind == 0 && kMediumFirst<kF>) {
         if (S.mb_entry < S.num_top && __builtin_popcountll(__builtin_amdgcn_read_exec()) <= RT_MB_LANES) {
             cb = medium_first_estimate<kF>(S, S.entries + S.mb_entry, r, g, k);
+#ifdef RT_LEAF_AUDIT
+            // audit build, RT_OPT_TUNE kModeMbShrink: an estimate half as far, so that the exact check
+            // fails wherever the walk finds nothing below it and the fallback (the hand-over) is exercised
+            if (mode & kModeMbShrink) cb *= 0.5f;
+#endif
             // B = C(1 + 2^-18) + 2 delta / min|d_a|: bvh_hit's inflated-entry margin te - delta * max|inv_a|
             // (the BVHs before the medium are translated only, so the ray's inverse direction is
             // theirs; the factor 2 and the 2^-18 cover the roundings of inv and of B itself)

@@ -454,3 +454,46 @@ def test_streaming_replay_pass_matches_oracle(cfg_name, stream, rt, orc):
                 assert st["segments"] == cnt["segments"]
         finally:
             ds.close()
+
+
+def test_medium_first_fallback_stays_exact():
+    # The medium-first bound walks the entries before the first medium with a bound
+    # from an f32 estimate of the scatter point, and hands the sample to the reference kernel when
+    # the exact values contradict the estimate. That fallback is rare with the real estimate; the
+    # audit build's RT_OPT_TUNE kModeMbShrink (bit 29) halves the estimate so that it fires on
+    # most segments inside the dense medium. A 1/256 C3 shard at 64 spp must still match the
+    # oracle bit for bit, and the launch log must show many more hand-overs than without it.
+    import subprocess
+    import sys
+    root = os.path.dirname(HERE)
+    lib = os.path.join(root, "raytracinginoneweekendinrust_amd", "_lib", "librtamd_audit.so")
+    assert os.path.exists(lib), "build() makes the audit library"
+    code = r'''
+import sys, json, numpy as np
+sys.path.insert(0, {root!r}); sys.path.insert(0, {oracle!r})
+import raytracinginoneweekendinrust_amd as rt, oracle_ffi as orc
+cfg = rt.CONFIGS["C3"]
+scene = rt.Scene.generate(cfg.scene, cfg.scene_seed)
+p = rt.render_params(cfg.width, cfg.height, 64, cfg.depth, background=cfg.background(), shard_index=101, shard_count=256)
+want = np.full(cfg.width * cfg.height * 3, np.nan, dtype=np.float32)
+_, cnt = orc.render(scene, cfg.camera(), p, out=want, threads=8)
+ds = rt.DeviceScene(scene)
+got, st = ds.render(cfg.camera(), p)
+ds.close()
+got = np.asarray(got).reshape(-1)
+m = ~np.isnan(want)
+print(json.dumps({{"equal": bool((got[m] == want[m]).all()), "segments": int(st["segments"]), "oracle": int(cnt["segments"])}}))
+'''.format(root=root, oracle=os.path.join(root, "oracle"))
+    counts = {}
+    for tune in ("0", str(1 << 29)):
+        env = dict(os.environ, RT_LIBRARY=lib)
+        r = subprocess.run([sys.executable, "-c", "import os, raytracinginoneweekendinrust_amd as rt\n"
+                            f"rt.set_option('tune', {tune}); rt.set_option('launch_log', 1)\n" + code],
+                           capture_output=True, text=True, env=env, timeout=600, cwd=root)
+        assert r.returncode == 0, r.stderr[-2000:]
+        res = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+        assert res["equal"], (tune, res)
+        assert res["segments"] == res["oracle"], (tune, res)
+        counts[tune] = sum(int(x.split("chunk")[1].split(":")[1].split()[0]) for x in r.stderr.splitlines()
+                           if "samples replayed" in x)
+    assert counts[str(1 << 29)] > 10 * max(counts["0"], 1), counts
