@@ -47,12 +47,32 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+IMPL_BYTES_PER_SAMPLE = 12.0  # the implementation's own sample-buffer record (written once, read once): not §8(d)
+
+
 def bytes_per_sample(counters: dict, spp: int) -> float:
-    """Algorithmic bytes per camera sample of trace_samples: the scene records the
-    reference algorithm touches (counted by the oracle) + the 12-byte radiance
-    record each sample writes to the HBM sample buffer + 12/spp framebuffer."""
+    """Algorithmic bytes per camera sample exactly as SURVEY.md §8(d) states them: the scene
+    records the reference algorithm touches (counted by the oracle's instrumented recursion)
+    + 12/spp framebuffer. The implementation's 12-byte sample-buffer record is NOT part of
+    it (reported apart as `impl_bytes_per_sample`)."""
     total = sum(BYTES[k] * counters[k] for k in BYTES)
-    return total / counters["samples"] + 12.0 + 12.0 / spp
+    return total / counters["samples"] + 12.0 / spp
+
+
+ISSUE_CEILING_TOL = 0.15  # roofline.bound = "valu" when the PMC issue fraction is within 15% of its ceiling
+
+
+def roofline_bound(valu) -> tuple:
+    """The kernel's bound as the committed PMC for this very library shows it: "valu" when the
+    SIMDs issue VALU in at least 85% of the quad-cycles the measured ceiling allows (the kernel
+    is then issue-bound, whatever its HBM rate), else "latency"; "hbm" (§8(d)'s nominal bound)
+    only when no PMC summary matches the loaded library."""
+    if not valu or valu.get("issue_quads") is None:
+        return "hbm", "no PMC summary for this library: §8(d)'s nominal HBM bound"
+    q, ceil = float(valu["issue_quads"]), float(valu.get("issue_quads_ceiling") or 0.94)
+    if q >= (1.0 - ISSUE_CEILING_TOL) * ceil:
+        return "valu", f"PMC: VALU issue in {q:.3f} of the quad-cycles, ceiling {ceil} (within 15%)"
+    return "latency", f"PMC: VALU issue {q:.3f} of the quad-cycles, below 85% of the {ceil} ceiling (waits dominate)"
 
 
 def host_nproc() -> int:
@@ -99,7 +119,7 @@ def cpu_threads() -> int:
     return max(1, n)
 
 
-PMC_DIRS = tuple(os.path.join(ROOT, "profiles", d) for d in ("r05", "r04", "r03", ""))
+PMC_DIRS = tuple(os.path.join(ROOT, "profiles", d) for d in ("r06", "r05", "r04", "r03", ""))
 
 
 def library_md5() -> str:
@@ -348,6 +368,8 @@ def main() -> int:
         if valu:
             valu = {k: v for k, v in valu.items() if k != "counters"}
         value = total_samples / wall_max / 1e6
+        bound, bound_why = roofline_bound(valu)
+        traffic_gbs = (traffic / (kernel_ms / 1e3) / 1e9) if traffic else None
         if cpu:
             cpu["gpu_over_cpu"] = value / cpu["value"]
             cpu["gpu_over_host_nproc_extrapolation"] = value / cpu["host_nproc_linear_extrapolation"]
@@ -386,21 +408,32 @@ def main() -> int:
             "image_finite": img_ok,
             "frame_sum": frame_sum,
             "frame_md5": frame_md5,
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "roofline": {"bound": bound, "bound_source": bound_why,
+                         "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
                          # the same rate against the XCD L2's measured shared-row rate (the scene's home)
                          "l2_peak": L2_PEAK_GBS, "l2_frac": (achieved / L2_PEAK_GBS) if achieved else None,
                          "achieved_is": "SURVEY.md §8(d) algorithmic bytes per sample (the reference algorithm's "
-                                        "scene reads, counted by the oracle) x samples / trace-kernel time: an "
-                                        "L2 scene-read rate (the scene is L2-resident), priced against HBM peak "
-                                        "as §8(d) asks; the kernel's measured limit is in `valu` (vector-ALU "
-                                        "lane throughput against the measured issue peak), not HBM",
-                         "traffic_GBs": (traffic / (kernel_ms / 1e3) / 1e9) if traffic else None,
+                                        "scene reads, counted by the oracle, + 12/spp framebuffer) x samples / "
+                                        "trace-kernel time: an L2 scene-read rate (the scene is L2-resident), "
+                                        "priced against HBM peak as §8(d) asks; the kernel's measured limit is in "
+                                        "`bound` / `valu` (vector-ALU issue against the measured ceiling), and its "
+                                        "real HBM use in `hbm_frac`",
+                         "traffic_GBs": traffic_gbs,
+                         # measured memory-side bytes (PMC) per launch / kernel time, against HBM peak
+                         "hbm_frac": (traffic_gbs / HBM_PEAK_GBS) if traffic_gbs else None,
                          "valu": valu,
                          "pmc_library_md5": md5,
-                         "kernel": "trace_samples", "kernel_ms": kernel_ms, "launches_per_step":
-                             trace_launches / args.steps, "step_device_ms": step_ms,
-                         "bytes_per_sample": b_sample, "samples_per_launch": samples_per_trace_launch},
+                         "kernel": "trace_samples", "kernel_ms": kernel_ms,
+                         # pipelined (N > 1): a launch's HIP events span the neighbouring frames' launches on
+                         # the other handles, so kernel_ms and the rates above are overlapped spans, not
+                         # comparable with the one-GPU line
+                         "kernel_ms_is": ("overlapped: frames in flight, each launch's events span the "
+                                          "concurrent launches on the other handles" if pipeline else
+                                          "per trace launch: HIP events on the launch stream"),
+                         "launches_per_step": trace_launches / args.steps, "step_device_ms": step_ms,
+                         "bytes_per_sample": b_sample, "impl_bytes_per_sample": IMPL_BYTES_PER_SAMPLE,
+                         "samples_per_launch": samples_per_trace_launch},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

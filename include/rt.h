@@ -304,7 +304,12 @@ int rt_bvh_build_order(const float* d_keys, uint32_t n, uint64_t seed, uint32_t*
  * variables: each switch below is process-wide, starts at its default, and changes only
  * through rt_set_option. None is needed for production renders.
  *   RT_OPT_TUNE             traversal mode bits (kernel.hip kMode*; default 0). Bit 16 sends
- *                           the replay pass through the literal reference kernel.
+ *                           the replay pass through the literal reference kernel. The product
+ *                           library accepts only bits that leave the image bits unchanged
+ *                           (kernel.hip kTuneExact: 1, 5, 6, 7, 16, 17, 21, 22, 24-27); any
+ *                           other bit (the inexact prune-all experiment, audit and ablation
+ *                           switches) is RT_ERR_INVALID there and honoured only by the
+ *                           diagnostic builds (librtamd_audit.so, librtamd_ablate.so).
  *   RT_OPT_GROUP            samples per batch (1..64; 0 = automatic, the default)
  *   RT_OPT_STACK_LDS        cap on the LDS part of the traversal stack, read at upload
  *                           (>= 1; 0 = the default 19 entries); deeper stacks spill to HBM

@@ -72,8 +72,14 @@ constexpr uint32_t kModeExact = 1u, kModeNoLeafBoxes = 2u, kModeNoPermLds = 32u,
 // handed-over sample after it); the tests cover both
 constexpr uint32_t kModeNoStream = 1u << 17;
 // EXPERIMENT ONLY (RT_OPT_TUNE, not exact): closest-hit pruning also on BVHs the proof does not
-// cover (triangles, moving spheres), to measure what an exact bound for them could gain.
+// cover (triangles, moving spheres), to measure what an exact bound for them could gain. Compiled
+// into the audit and ablation builds only: the product library rejects the bit (kTuneAccepted).
 constexpr uint32_t kModePruneAllExp = 1u << 20;
+#if defined(RT_LEAF_AUDIT) || defined(RT_ABLATE)
+constexpr bool kPruneAllExpBuild = true;
+#else
+constexpr bool kPruneAllExpBuild = false;
+#endif
 // Block order: a shard's blocks are taken last block first (bottom image rows first), so the
 // upper rows, which in every BASELINE framing hold the background and end their paths after a
 // segment or two, are the work left when the pool runs dry and the drain is short (one rank of
@@ -84,6 +90,27 @@ constexpr uint32_t kModeBlocksForward = 1u << 21;
 constexpr uint32_t kModeW4 = 1u << 22;
 // MbShrink (RT_OPT_TUNE, audit build only): halves the medium-first estimate (world_hit)
 [[maybe_unused]] constexpr uint32_t kModeMbShrink = 1u << 29;
+// The RT_OPT_TUNE bits a build honours. Every bit of the product library leaves the image bits
+// unchanged (instance choice, block order, replay-pass form, leaf postponement's q in bits 24-27,
+// switching exact shortcuts off); rt_set_option refuses any other bit with RT_ERR_INVALID, so no
+// caller can leave parity through the C ABI (the boundary contract: renderer.rs:42-52 has no knob
+// that changes results). The audit, ablation and A/B builds add their diagnostic bits.
+constexpr uint32_t kTuneExact = kModeNoLeafBoxes | kModeNoPermLds | kModeW3 | kModeNoPretest | kModeReplayRef |
+                                kModeNoStream | kModeBlocksForward | kModeW4 | (15u << 24);
+constexpr uint32_t kTuneAccepted = kTuneExact
+#if defined(RT_LEAF_AUDIT) || defined(RT_ABLATE)
+                                   | kModePruneAllExp
+#endif
+#ifdef RT_LEAF_AUDIT
+                                   | kModeMbShrink
+#endif
+#ifdef RT_ABLATE
+                                   | (31u << 8)  // kAb* below
+#endif
+#ifdef RT_EXP_STRIDE
+                                   | (1u << 23)
+#endif
+    ;
 #ifdef RT_ABLATE
 // Ablation build (librtamd_ablate.so, diagnostics only): RT_OPT_TUNE bits that run a
 // piece of work twice (results of the copy discarded through an opaque test),
@@ -1239,7 +1266,8 @@ template <int kKind, uint32_t kF, bool kSusp>
 RT_DEV bool bvh_run(const DevScene& S, float delta, const f4* wrapper, const Ray& r, V inv, float tmin, float& closest,
                     uint32_t& hit_code, uint32_t* stk, uint32_t mode, Trav& tv, uint32_t susp) {
     const float tmax_entry = tv.tmax_entry;
-    const bool prune = (__float_as_uint(ld4c(wrapper + 7).w) & rtdev::kBvhPrunable) != 0u || (mode & kModePruneAllExp);
+    const bool prune = (__float_as_uint(ld4c(wrapper + 7).w) & rtdev::kBvhPrunable) != 0u ||
+                       (kPruneAllExpBuild && (mode & kModePruneAllExp));
     const float dmi = delta * fmaxf(fmaxf(__builtin_fabsf(inv.x), __builtin_fabsf(inv.y)), __builtin_fabsf(inv.z));
     const bool leaf_boxes = prune && !(mode & kModeNoLeafBoxes);
     // Byte offsets of each axis's near-plane row in a node (min.a rows 0-2, max.a rows 3-5;
@@ -1711,9 +1739,6 @@ RT_DEV bool entry_geom_hit(const DevScene& S, float delta, const DevEntry* E, Ra
 // leaves it unscattered by the estimate).
 #ifndef RT_MEDIUM_FIRST
 #define RT_MEDIUM_FIRST 1
-#endif
-#ifndef RT_MB_LANES
-#define RT_MB_LANES 64  // bound only waves with at most this many active lanes
 #endif
 // Compiled into the sphere-BVH preset with marble textures (the book-2 final scene's, C3): same box,
 // same bits, C3 93.4 -> 88.9 ms per 100-spp frame and one rank of 8 60.1 -> 57.2 ms; the BVH-only
@@ -2282,7 +2307,9 @@ RT_DEV bool world_hit(const DevScene& S, float delta, const Ray& r, Rng& g, cons
     float closest = kInf;
     float cb = kInf;  // the medium-first bound C (medium_first_estimate)
     if constexpr (kKind == 0 && kMediumFirst<kF>) {
-        if (S.mb_entry < S.num_top && __builtin_popcountll(__builtin_amdgcn_read_exec()) <= RT_MB_LANES) {
+        // (every wave takes the bound: bounding only the waves with few active lanes, the drain's,
+        // gained nothing over no bound)
+        if (S.mb_entry < S.num_top) {
             cb = medium_first_estimate<kF>(S, S.entries + S.mb_entry, r, g, k);
 #ifdef RT_LEAF_AUDIT
             // audit build, RT_OPT_TUNE kModeMbShrink: an estimate half as far, so that the exact check
@@ -3756,16 +3783,18 @@ int rt_render_launch_camera(rt_scene_handle s, const rt_camera* camera, const rt
     }
     if (s->fast_waves == 4) dp.tune |= kModeNoPermLds;
     // LDS per wave: the kernel's traversal stack, then the Perlin tables
-    DevScene dev_ref = s->dev;
-    dev_ref.stack_depth = s->stack_ref;
     const size_t perm_lds =
         s->dev.perm_bytes != 0u && s->dev.perm_bytes <= kPermLdsMax && !(dp.tune & kModeNoPermLds) ? s->dev.perm_bytes : 0u;
     size_t lds = (size_t)s->dev.stack_depth * 128u * sizeof(uint32_t) + perm_lds;
-    // the flat-list preset stages a small scene's materials and textures behind the stack
+    // the flat-list preset stages a small scene's materials and textures behind the stack (the fast
+    // kernel's launch only: the reference and replay launches below reserve no LDS for them)
     const size_t mt_bytes = (size_t)(s->dev.num_mats + s->dev.num_texs) * 32u;
     const bool mt_stage = RT_MT_LDS && s->features == 0u && perm_lds == 0u && mt_bytes <= kMtLdsMax;
     s->dev.mt_lds = mt_stage ? (uint32_t)mt_bytes : 0u;
     if (mt_stage) lds += mt_bytes;
+    DevScene dev_ref = s->dev;
+    dev_ref.stack_depth = s->stack_ref;
+    dev_ref.mt_lds = 0u;
     size_t lds_ref = (size_t)dev_ref.stack_depth * 128u * sizeof(uint32_t) + perm_lds;
     if ((dp.flags & RT_FLAG_HRPP) && s->dev.hrpp_npred) {  // the experiment: reference kernel + predictors
         dp.flags |= RT_FLAG_EXACT_BVH;
@@ -3878,6 +3907,7 @@ int rt_render_launch_camera(rt_scene_handle s, const rt_camera* camera, const rt
                 // the replay pass: fast traversal except for the rays that were handed over
                 DevScene dev_rp = s->dev;
                 dev_rp.stack_depth = std::max(s->dev.stack_depth, s->stack_ref);
+                dev_rp.mt_lds = 0u;  // (only the fast kernel's launch stages them)
                 const size_t lds_rp = (size_t)dev_rp.stack_depth * 128u * sizeof(uint32_t) + perm_lds;
                 if (stream_rp) {  // streaming: takes the handed-over samples during the fast kernel's drain
                     // few waves: each polls the counters while it waits (3072 pollers slowed the
@@ -4104,7 +4134,9 @@ int rt_set_option(int option, int64_t value) {
     if (option < 0 || option >= RT_OPT_COUNT) return rthost::set_error(RT_ERR_INVALID, "unknown option");
     bool ok = true;
     switch (option) {
-        case RT_OPT_TUNE: ok = value >= 0 && value <= 0xffffffffll; break;
+        case RT_OPT_TUNE:  // only the bits this build honours (the product: exact ones only)
+            ok = value >= 0 && value <= 0xffffffffll && ((uint64_t)value & ~(uint64_t)kTuneAccepted) == 0u;
+            break;
         case RT_OPT_GROUP: ok = value >= 0 && value <= 64; break;
         case RT_OPT_STACK_LDS: ok = value >= 0 && value <= 96; break;
         case RT_OPT_SAMPLE_BUFFER_MB: ok = value >= 0 && value <= (1ll << 30); break;

@@ -173,6 +173,43 @@ def test_diagnostic_options_are_explicit(rt):
     assert _capi.lib.rt_set_option(99, 0) == -1
 
 
+def _load_copy(path, tmp_path, name):
+    import shutil
+    copy = tmp_path / name
+    shutil.copyfile(path, copy)
+    lib = C.CDLL(str(copy))
+    lib.rt_set_option.argtypes = [C.c_int, C.c_int64]
+    lib.rt_get_option.argtypes = [C.c_int, C.POINTER(C.c_int64)]
+    return lib
+
+
+def test_product_refuses_tune_bits_that_leave_parity(rt, tmp_path):
+    # The product library honours only RT_OPT_TUNE bits that keep the image bits (instance choice,
+    # block order, replay-pass form, exact shortcuts off, leaf postponement's q): the inexact
+    # prune-all experiment (bit 20), the audit's estimate shrink (bit 29), the ablation bits (8-12),
+    # the A/B block-stride bit (23) and the unused kModeExact bit 0 are RT_ERR_INVALID there, and
+    # the option keeps its previous value. The audit build (the diagnostic library) still takes its bits.
+    from raytracinginoneweekendinrust_amd import _capi
+    lib = _load_copy(_capi.LIB_PATH, tmp_path, "librtamd_product_copy.so")
+    tune = _capi.OPTIONS["tune"]
+    val = C.c_int64(-1)
+    for bit in (0, 8, 9, 10, 11, 12, 20, 23, 29, 30, 31):
+        assert lib.rt_set_option(tune, 1 << bit) == -1, bit  # RT_ERR_INVALID
+        assert lib.rt_get_option(tune, C.byref(val)) == 0 and val.value == 0, bit
+    for bits in (1 << 1, 1 << 5, 1 << 6, 1 << 7, 1 << 16, 1 << 17, 1 << 21, 1 << 22, 15 << 24, 3 << 24 | 1 << 16):
+        assert lib.rt_set_option(tune, bits) == 0, hex(bits)
+        assert lib.rt_get_option(tune, C.byref(val)) == 0 and val.value == bits
+    assert lib.rt_set_option(tune, 0) == 0
+    audit = os.path.join(os.path.dirname(_capi.LIB_PATH), "librtamd_audit.so")
+    alib = _load_copy(audit, tmp_path, "librtamd_audit_copy.so")
+    for bits in (1 << 20, 1 << 29, 1 << 20 | 1 << 29 | 1 << 21):
+        assert alib.rt_set_option(tune, bits) == 0, hex(bits)
+    assert alib.rt_set_option(tune, 1 << 8) == -1  # ablation bits: librtamd_ablate.so only
+    assert alib.rt_set_option(tune, 0) == 0
+    src = open(os.path.join(ROOT, "raytracinginoneweekendinrust_amd", "csrc", "kernel.hip")).read()
+    assert "(kPruneAllExpBuild && (mode & kModePruneAllExp))" in src
+
+
 def test_abi_layouts_match_the_header_and_the_ctypes_mirror(tmp_path):
     # include/rt.h asserts its struct layouts (RT_LAYOUT_ASSERT) on every C / C++ compile; the
     # ctypes mirror and INTEGRATION.md's #[repr(C)] structs must describe the same bytes.
