@@ -37,6 +37,11 @@ constexpr uint32_t kLeafMedium = 6u;   // hit identifier of a ConstantMedium sca
 constexpr uint32_t kChildEmpty = 0xffffffffu;  // second child of a 1-object node (bvh.rs:261-264)
 constexpr uint32_t kMaxIndex = 0x0fffffffu;
 constexpr uint32_t kBvhPrunable = 1u;  // wrapper-node flag: closest-hit box pruning is exact for this BVH
+// BVH4 wrapper flag (rank[3], with kBvhPrunable): every leaf is a Tri (the BVH2 wrapper's
+// kBvh2TriOnly below, for the fast traversal). Such a BVH is never prunable, so its slab tests
+// use no delta-inflation, and the fast kernel traverses it also with a zero direction component
+// (kernel.hip ray_route).
+constexpr uint32_t kBvhTriOnly = 2u;
 // BVH2 wrapper flag (nodes2 wrapper row 3 .w): every leaf is a Tri. Möller-Trumbore
 // (triangle.rs:32-92) rejects any ray with a NaN origin or direction component (a NaN
 // reaches t, and !(t > EPSILON) rejects it), so such a BVH returns no hit for that ray

@@ -1204,6 +1204,49 @@ constexpr uint32_t kSuspMinTrips = RT_SUSP_MIN_TRIPS;
 template <int kKind, uint32_t kF, bool kSusp>
 RT_DEV bool bvh_run(const DevScene& S, float delta, const f4* wrapper, const Ray& r, V inv, float tmin, float& closest,
                     uint32_t& hit_code, uint32_t* stk, uint32_t mode, Trav& tv, uint32_t susp);
+// Which traversal a ray takes into a BVH (bvh_hit, world_walk, the replay pass).
+// kRayFast: the fast BVH4 traversal is exact for it. Its packed slab test (child_keys4_nf)
+// forms each child's interval with max / min, and those equal aabb.rs:28-41's sequential
+// `if t0 > t_min {t0} else {t_min}` clamps as long as the only NaN slab values are the ones the
+// reference's comparisons ignore too: maxnum / minnum return the other operand of a quiet NaN,
+// and the reference keeps t_min / t_max unchanged on a NaN t0 / t1; the empty slots' infinite
+// planes must never give NaN, and the entry t_max must not be NaN (every reference box test
+// passes with t_max = NaN, and HittableList::hit still takes the BVH's hit). So:
+// * every BVH: a finite origin, 0 < |1/d| < inf on every axis (no NaN slab value at all, and
+//   delta * max|1/d| stays finite for the exact-pruning margin), and a non-NaN entry t_max;
+// * a triangle-only BVH (kBvhTriOnly: never prunable, no delta margin, and Tri::hit never
+//   returns a NaN t): also a zero or denormal direction component. Then 1/d = +-inf and the only
+//   NaN slab values are 0 * inf on a plane through the origin; the empty slots' planes give
+//   (+-inf - o) * +-inf = +-inf. Round 5 handed these rays over (C4: ~15,500 samples a frame,
+//   whose re-traced paths were the 23-50 ms replay tail).
+// kRayNoHit: a triangle-only BVH and a NaN in the ray: Moller-Trumbore (triangle.rs:32-92) takes
+// no such ray (a NaN reaches t and !(t > EPSILON) rejects it), so the BVH returns no hit whatever
+// its boxes do (bvh_hit_reference's kBvh2TriOnly answer, without the walk).
+// kRayHandOver: everything else goes to the literal recursion (a zero direction component in a
+// BVH with rects, whose 0/0 = NaN hits make the tree-min order-dependent; a non-finite origin or
+// direction; a NaN closest_so_far, e.g. from a 0/0 rect hit earlier in the list whose plane axis
+// the BVH's own frame rotated away).
+constexpr uint32_t kRayFast = 0u, kRayHandOver = 1u, kRayNoHit = 2u;
+template <uint32_t kF>
+RT_DEV uint32_t ray_route(const Ray& r, V inv, float tmax_entry, const f4* wrapper, uint32_t mode) {
+    const float ax = __builtin_fabsf(inv.x), ay = __builtin_fabsf(inv.y), az = __builtin_fabsf(inv.z);
+    const bool ofin = __builtin_fabsf(r.o.x) < kInf && __builtin_fabsf(r.o.y) < kInf && __builtin_fabsf(r.o.z) < kInf;
+    const bool tnum = tmax_entry == tmax_entry;
+    if (ax > 0.0f && ax < kInf && ay > 0.0f && ay < kInf && az > 0.0f && az < kInf && ofin && tnum) return kRayFast;
+    if constexpr ((kF & kFTri) != 0u) {
+        if ((__float_as_uint(ld4c(wrapper + 7).w) & rtdev::kBvhTriOnly) != 0u &&
+            !(kPruneAllExpBuild && (mode & kModePruneAllExp))) {
+            if (r.o.x != r.o.x || r.o.y != r.o.y || r.o.z != r.o.z || r.d.x != r.d.x || r.d.y != r.d.y ||
+                r.d.z != r.d.z)
+                return kRayNoHit;
+            const bool dfin =
+                __builtin_fabsf(r.d.x) < kInf && __builtin_fabsf(r.d.y) < kInf && __builtin_fabsf(r.d.z) < kInf;
+            if (dfin && ofin && tnum) return kRayFast;
+        }
+    }
+    return kRayHandOver;
+}
+
 template <int kKind, uint32_t kF = kFAll>
 RT_DEV bool bvh_hit(const DevScene& S, float delta, uint32_t root, const Ray& r, float tmin, float& closest,
                     uint32_t& hit_code, uint32_t* stk, uint32_t mode, bool& replay) {
@@ -1220,25 +1263,21 @@ RT_DEV bool bvh_hit(const DevScene& S, float delta, uint32_t root, const Ray& r,
         }
         return bvh_hit_reference(S, w2, r, q, inv, tmin, closest, hit_code, stk);
     }
-    // Only rays with 0 < |1/d| < inf on every axis stay here: a zero component
-    // (1/d = inf: NaN rect hits), a denormal one (1/d = inf) or a non-finite one
-    // (1/d = 0 or NaN, e.g. H = 1 images divide by H - 1 = 0 in renderer.rs:141)
-    // would give 0 * inf = NaN slab values, which the packed child test and the
-    // empty slots' infinite boxes must never see. The reference kernel takes them.
+    // The fast traversal takes only the rays ray_route admits (a zero, denormal or non-finite
+    // direction component would give 0 * inf = NaN slab values, which the packed child test, the
+    // pruning margin and the empty slots' infinite boxes must not see, except in a triangle-only
+    // BVH; e.g. H = 1 images divide by H - 1 = 0 in renderer.rs:141). A non-finite origin is
+    // handed over too: a NaN rect hit leaves a NaN origin for the next bounce, which the replay
+    // pass can meet after a bounce the fast kernel never traced. The reference kernel takes them.
     {
-        const float ax = __builtin_fabsf(inv.x), ay = __builtin_fabsf(inv.y), az = __builtin_fabsf(inv.z);
-        // A non-finite origin is handed over too: a NaN rect hit (above) leaves a NaN
-        // origin for the next bounce, which the replay pass can meet after a bounce the
-        // fast kernel never traced.
-        const bool fast = ax > 0.0f && ax < kInf && ay > 0.0f && ay < kInf && az > 0.0f && az < kInf &&
-                          __builtin_fabsf(r.o.x) < kInf && __builtin_fabsf(r.o.y) < kInf &&
-                          __builtin_fabsf(r.o.z) < kInf;
+        const uint32_t route = ray_route<kF>(r, inv, closest, wrapper, mode);
+        if (route == kRayNoHit) return false;
         if constexpr (kKind == 3) {
-            if (!fast)
+            if (route == kRayHandOver)
                 return bvh_hit_reference(S, __float_as_uint(ld4c(wrapper + 7).z), r, to_d(r), inv, tmin, closest, hit_code,
                                          stk);
         }
-        if (!fast) {
+        if (route == kRayHandOver) {
             replay = true;
             return false;
         }
@@ -2400,13 +2439,14 @@ RT_DEV void world_walk(const DevScene& S, float delta, const Ray& ray, Rng& g, c
             const f4* wrapper = S.nodes + (size_t)root * rtdev::kBvhNodeF4;
             const V inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
             if (!w.resume) {  // bvh_hit's hand-over rule (NaN-prone rays go to the reference kernel)
-                const float ax = __builtin_fabsf(inv.x), ay = __builtin_fabsf(inv.y), az = __builtin_fabsf(inv.z);
-                const bool fast = ax > 0.0f && ax < kInf && ay > 0.0f && ay < kInf && az > 0.0f && az < kInf &&
-                                  __builtin_fabsf(r.o.x) < kInf && __builtin_fabsf(r.o.y) < kInf &&
-                                  __builtin_fabsf(r.o.z) < kInf;
-                if (!fast) {
+                const uint32_t route = ray_route<kF>(r, inv, w.closest, wrapper, mode);
+                if (route == kRayHandOver) {
                     replay = true;
                     w.pos = S.num_top + 1u;  // abandoned: the sample is re-traced by the reference kernel
+                    continue;
+                }
+                if (route == kRayNoHit) {  // a triangle-only BVH takes no NaN ray: no hit, next entry
+                    w.pos = e + 1u;
                     continue;
                 }
                 w.tv = Trav{root, 0u, 0u, w.closest, false, kNoNode};

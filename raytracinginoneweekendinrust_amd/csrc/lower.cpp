@@ -898,7 +898,8 @@ class Lowerer {
         };
         // wrapper: slot 0 = the root (its box is tested on entry, bvh.rs:370);
         // its rank[3] carries the BVH's flags
-        put(base, {Slot{true, wroot | 0x40000000u, tn[troot].box, 0u}}, prunable ? rtdev::kBvhPrunable : 0u);
+        put(base, {Slot{true, wroot | 0x40000000u, tn[troot].box, 0u}},
+            (prunable ? rtdev::kBvhPrunable : 0u) | (tri_only && !prunable ? rtdev::kBvhTriOnly : 0u));
         s_->nodes[(size_t)base * rtdev::kBvhNodeF4 + 7].z = bitsf(base2);  // wrapper rank[2]: the BVH2 wrapper
         if (predictor) {  // Bvh::with_predictor (bvh.rs:69-80): HRPP side data
             // The predictor table stores, per ray hash, "leaf nodes" (GO_UP_LEVEL = 0,

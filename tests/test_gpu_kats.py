@@ -40,6 +40,43 @@ def test_sphere_rs_get_uv_examples_on_device(rt, orc, p, uv):  # sphere.rs:37-40
     np.testing.assert_array_equal(got, np.array(orc.sphere_uv(p), dtype=np.float32))
 
 
+def test_zero_direction_components_fast_equals_exact(rt, orc):
+    # The fast test on rays with exactly zero (+0 / -0) direction components (1/d = +-inf), as the
+    # triangle-only BVHs take them since round 6 (kernel.hip ray_route): slab values are +-inf, or
+    # 0 * inf = NaN where the origin lies on a slab plane, which aabb.rs:28-41's comparisons ignore
+    # and max / min ignore too. aabb.rs:73-97's boxes with the axis-parallel rays of its own tests,
+    # then random boxes whose planes the origins sit on; hit flag and entry equal the exact test's,
+    # and both equal the oracle's restatement of aabb.rs.
+    rng = np.random.default_rng(17)
+    cases = [[-1, -1, 1, 1, 1, 2, 0, 0, 0, 0, 0, 1, 0.0, 5.0], [1, 1, 1, 2, 2, 2, 0, 0, 0, 0, 0, 1, 0.0, 5.0],
+             [-1, -1, 1, 1, 1, 2, 0, 0, 0, -0.0, 0.0, 1, 0.0, 5.0], [-1, -1, 1, 1, 1, 2, 1, 1, 0, 0, 0, 1, 0.0, 5.0],
+             [-1, -1, 1, 1, 1, 2, 1, -1, 0, 0, -0.0, 1, 0.0, float("inf")]]
+    n = 6000
+    mn = rng.integers(-8, 8, (n, 3)).astype(np.float32)
+    mx = mn + rng.integers(0, 5, (n, 3)).astype(np.float32)
+    o = rng.integers(-10, 10, (n, 3)).astype(np.float32)
+    pick = rng.integers(0, 3, (n, 3))  # origin coordinates on the min plane, the max plane or elsewhere
+    o = np.where(pick == 0, mn, np.where(pick == 1, mx, o)).astype(np.float32)
+    d = ((mn + mx) / 2 - o + rng.normal(scale=1.0, size=(n, 3))).astype(np.float32)
+    zero = rng.random((n, 3)) < 0.45
+    sign = rng.random((n, 3)) < 0.5
+    d = np.where(zero, np.where(sign, np.float32(-0.0), np.float32(0.0)), d).astype(np.float32)
+    zero[:, 0] |= ~zero.any(axis=1)  # at least one zero component per ray
+    d[:, 0] = np.where(zero[:, 0] & (d[:, 0] != 0), np.float32(0.0), d[:, 0])
+    t = np.stack([rng.uniform(0, 0.3, n), np.where(rng.random(n) < 0.3, np.inf, rng.uniform(0.5, 30, n))],
+                 axis=1).astype(np.float32)
+    cases = np.concatenate([np.array(cases, dtype=np.float32), np.concatenate([mn, mx, o, d, t], axis=1)])
+    exact = rt.device_kat(0, cases)
+    fast = rt.device_kat(1, cases)
+    want = np.array([orc.aabb_hit(c[0:3], c[3:6], c[6:9], c[9:12], c[12], c[13]) for c in cases])
+    assert exact[0, 0] == 1.0 and exact[1, 0] == 0.0  # aabb.rs:73-97 hits / misses
+    np.testing.assert_array_equal(exact[:, 0] == 1.0, want)
+    np.testing.assert_array_equal(fast[:, 0], exact[:, 0])
+    hit = exact[:, 0] == 1.0
+    assert 0.1 < hit.mean() < 0.9, hit.mean()
+    np.testing.assert_array_equal(fast[hit, 1], np.minimum(exact[hit, 1], np.float32(3.4028235e38)))
+
+
 def test_random_boxes_device_equals_oracle_and_fast_equals_exact(rt, orc):
     rng = np.random.default_rng(9)
     n = 20000

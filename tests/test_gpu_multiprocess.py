@@ -28,10 +28,10 @@ def _port():
     return p
 
 
-def _bench(args, launcher=()):
+def _bench(args, launcher=(), timeout=240):
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
     r = subprocess.run([*launcher, os.path.join(ROOT, "bench.py"), *args], capture_output=True, text=True,
-                       env=env, timeout=240, cwd=ROOT)
+                       env=env, timeout=timeout, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout[-2000:]
@@ -65,8 +65,29 @@ def test_two_rank_bench_back_to_back_frames_over_both_transports():
         assert two["frame_md5"] == one["frame_md5"], transport
 
 
+def test_eight_rank_bench_rehearsal_on_one_gpu():
+    """The driver's 8-GPU command shape, rehearsed with 8 processes sharing this box's GPU
+    (bench.py maps LOCAL_RANK onto the visible GPUs): 8 gloo ranks, frames in flight on three
+    scene handles per rank (--pipeline auto is on for N > 1, RT_FLAG_FRAMES_IN_FLIGHT), 1/8 of
+    the C1 frame's blocks per rank, gathered to rank 0 inside the timed region over the IPC pull
+    (7 peers, 3 handles each: 24 scenes on one device) and over the /dev/shm bounce. Rank 0's
+    frame after warmup 1 + 2 timed steps is the one-process frame bit for bit."""
+    common = ["--config", "C1", "--steps", "2", "--warmup", "1", "--no-cpu-baseline"]
+    one = _bench(common, (sys.executable,))
+    for transport in ("ipc", "shm"):
+        eight = _bench(["--gpus", "8", "--gather", transport, *common],
+                       (sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+                        "--master-addr", "127.0.0.1", "--master-port", str(_port())), timeout=420)
+        assert eight["n_gpus"] == 8 and eight["scaling"] == "strong"
+        assert eight["config"]["gather"] == transport
+        assert eight["config"]["pipeline"], "frames in flight are on for N > 1"
+        assert eight["frame_md5"] == one["frame_md5"], transport
+        assert eight["image_finite"]
+
+
 @pytest.mark.parametrize("transport,world,lag", [("ipc", 2, False), ("ipc", 3, False), ("shm", 2, False),
-                                                 ("ipc", 2, True), ("shm", 2, True)])
+                                                 ("ipc", 2, True), ("shm", 2, True), ("ipc", 8, False),
+                                                 ("shm", 8, False), ("ipc", 8, True)])
 def test_frame_gather_position_coded_frames(transport, world, lag, tmp_path):
     """FrameGather driven directly: 5 steps (both slots reused twice), a ragged 203 x 117
     frame whose every float is distinct and changes each step; rank 0's frame must equal
@@ -79,7 +100,7 @@ def test_frame_gather_position_coded_frames(transport, world, lag, tmp_path):
                         "--master-addr", "127.0.0.1", "--master-port", str(_port()),
                         os.path.join(ROOT, "tests", "gather_worker.py"), transport, "203", "117", "5", str(out),
                         *(["lag"] if lag else [])],
-                       capture_output=True, text=True, env=env, timeout=240, cwd=ROOT)
+                       capture_output=True, text=True, env=env, timeout=240 if world < 8 else 420, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     res = json.loads(out.read_text())
     assert res["transport"] == transport and res["world"] == world and res["lag"] == lag

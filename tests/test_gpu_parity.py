@@ -210,6 +210,82 @@ def test_suspending_walk_matches_oracle(w, h, spp, rt, orc):
     assert st["segments"] == cnt["segments"]
 
 
+def _planar_basis(rt, case):
+    """A constructed Camera (src/camera.rs:6-27's nine fields) whose every camera ray has an
+    exactly zero direction component: origin and lower-left corner share that coordinate,
+    horizontal and vertical have none, no lens. "zero_dx": the rays fan in the plane x = 278
+    through C4's Cornell box and mesh (cornell_boundaries + the mesh at (325, 0, 200),
+    src/main.rs:688-743, 791-802). "nan_closest": they fan in the back wall's plane z = 555, so
+    the back wall (xy_rect k = 555, the last rect before the mesh) gives every camera ray
+    (k - o) / d = 0 / 0 = NaN, which rectangle.rs:36-65 accepts whatever closest_so_far was."""
+    if case == "zero_dx":
+        return rt.CameraBasis(origin=(278.0, 278.0, -800.0), horizontal=(0.0, 0.0, 700.0),
+                              vertical=(0.0, 556.0, 0.0), lower_left_corner=(278.0, 0.0, 0.0),
+                              u=(0.0, 0.0, 1.0), v=(0.0, 1.0, 0.0), lens_radius=0.0, time_start=0.0, time_end=0.0)
+    return rt.CameraBasis(origin=(278.0, 278.0, 555.0), horizontal=(556.0, 0.0, 0.0),
+                          vertical=(0.0, 556.0, 0.0), lower_left_corner=(0.0, 0.0, 555.0),
+                          u=(1.0, 0.0, 0.0), v=(0.0, 1.0, 0.0), lens_radius=0.0, time_start=0.0, time_end=0.0)
+
+
+@pytest.mark.parametrize("case", ["zero_dx", "nan_closest"])
+@pytest.mark.parametrize("suspend", [True, False])
+def test_zero_direction_component_on_the_triangle_bvh(case, suspend, rt, orc, capfd):
+    # Since round 6 the fast traversal takes rays with a zero direction component into a
+    # triangle-only BVH (kernel.hip ray_route): 1/d = inf, and the only NaN slab values, 0 * inf
+    # on a plane through the origin, are ignored by max / min exactly as aabb.rs:28-41's
+    # comparisons ignore them. "zero_dx": every camera ray has d.x == 0 and crosses the mesh;
+    # none is handed over any more. "nan_closest": every camera ray takes the back wall's
+    # 0 / 0 = NaN hit, so the mesh BVH is entered with a NaN closest_so_far (every reference box
+    # test passes then): every sample goes to the reference kernel. Both match the oracle bit for
+    # bit, segment counts included, through the suspending walk (the product's triangle preset)
+    # and through the all-features instance (`suspend` False: the scene gets a sphere run).
+    cfg = rt.CONFIGS["C4"]
+    scene = rt.Scene.generate(cfg.scene, cfg.scene_seed) if suspend else _c4_with_spheres(rt)
+    basis = _planar_basis(rt, case)
+    params = rt.render_params(48, 36, 3, 8, background=cfg.background(), seed=3)
+    want, cnt = orc.render(scene, basis, params)
+    capfd.readouterr()
+    with rt.options(launch_log=1):
+        got, st = gpu_render(rt, scene, basis, params)
+    err = capfd.readouterr().err
+    np.testing.assert_array_equal(got, want)
+    assert st["segments"] == cnt["segments"]
+    replayed = sum(int(x.split("chunk")[1].split(":")[1].split()[0]) for x in err.splitlines()
+                   if "samples replayed" in x)
+    if case == "zero_dx":
+        assert replayed == 0, err[-2000:]
+    else:
+        assert replayed == 48 * 36 * 3, (replayed, err[-2000:])
+
+
+def _c4_with_spheres(rt):
+    """cornell_boundaries + a triangle mesh BVH (a tetrahedral fan around (325, 100, 200)) + a
+    top-level sphere run, built through SceneBuilder so that the scene has spheres and
+    triangles (the all-features instance)."""
+    b = rt.SceneBuilder()
+    red = b.lambertian_from_color((0.65, 0.05, 0.05))
+    white = b.lambertian_from_color((0.73, 0.73, 0.73))
+    green = b.lambertian_from_color((0.12, 0.45, 0.15))
+    light = b.diffuse_light_from_color((15.0, 15.0, 15.0))
+    w = rt.HittableList()
+    w.add(b.yz_rect(0, 555, 0, 555, 555, green))
+    w.add(b.yz_rect(0, 555, 0, 555, 0, red))
+    w.add(b.xz_rect(213, 343, 227, 332, 554, light))
+    w.add(b.xz_rect(0, 555, 0, 555, 0, white))
+    w.add(b.xz_rect(0, 555, 0, 555, 555, white))
+    w.add(b.xy_rect(0, 555, 0, 555, 555, white))
+    mesh = rt.HittableList()
+    rng = np.random.default_rng(11)
+    for _ in range(300):
+        c = rng.uniform((180, 20, 60), (470, 300, 340))
+        e = rng.uniform(-40, 40, size=(2, 3))
+        mesh.add(b.tri(tuple(c), tuple(c + e[0]), tuple(c + e[1]), white))
+    w.add(b.translate(b.bvh(mesh, 0.0, 1.0, axis_seed=4), (0.0, 0.0, 0.0)))
+    for i in range(10):
+        w.add(b.sphere((1000.0 + 10 * i, 2000.0, 3000.0), 1.0, white))
+    return b.finish(w)
+
+
 # --- sharding / determinism (the multi-GPU decomposition) ---------------------------
 @pytest.mark.parametrize("n", [2, 3, 8])
 def test_gpu_shards_compose_bit_identically(n, rt):
