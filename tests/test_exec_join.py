@@ -75,14 +75,19 @@ def test_build_guard_passes_the_product_and_the_audit_build():
     ge.exec_join_guard(paths)
 
 
-def test_build_guard_refuses_the_live_fixture_when_it_is_miscompiled():
+def test_build_guard_refuses_the_live_fixture_when_it_is_miscompiled(tmp_path):
     path = os.path.join(LIB, "librtamd_rngdiv.so")
     assert os.path.exists(path), "make -C raytracinginoneweekendinrust_amd/csrc rngdiv (__graft_entry__.build())"
     found = ejc.check_library(path)
     if not found:
         pytest.skip("this compiler no longer splits the Rng buffer at the fixture's join (reported, not required)")
+    # (on a copy: the guard moves a flagged library aside, so that nothing loads it afterwards)
+    import shutil
+    copy = tmp_path / "librtamd_rngdiv_copy.so"
+    shutil.copyfile(path, copy)
     with pytest.raises(RuntimeError, match="EXEC-join miscompile"):
-        ge.exec_join_guard([path])
+        ge.exec_join_guard([str(copy)])
+    assert not copy.exists() and (tmp_path / "librtamd_rngdiv_copy.so.miscompiled").exists()
     # whatever the allocator splits there is a plain copy into a register, in a fast-kernel instance
     for fn, _, what in found:
         assert kr.readable(fn).startswith("trace_samples<0,"), (fn, what)
