@@ -136,6 +136,9 @@ __device__ unsigned long long g_tp_hist[kTpBuckets];
 constexpr uint32_t kRoleEvents = 4096;
 __device__ unsigned long long g_role_ev[2 * kRoleEvents];
 __device__ unsigned g_role_n;
+// block-row band [g_prof_rows[0], g_prof_rows[1]) the profiling build renders (rt_prof_rows; the
+// other units are claimed and skipped): the region profile of one band of the image
+__device__ uint32_t g_prof_rows[2] = {0u, 0xffffffffu};
 __device__ __forceinline__ void role_event(uint32_t what) {
     const unsigned i = atomicAdd(&g_role_n, 1u);
     if (i < kRoleEvents) {
@@ -707,6 +710,10 @@ constexpr uint32_t kFSusp = 64u;
 #ifndef RT_SHARE
 #define RT_SHARE 1
 #endif
+// RT_SHARE_TRI (A/B): the triangle preset without the suspending walk, traversing across lanes
+#ifndef RT_SHARE_TRI
+#define RT_SHARE_TRI 0
+#endif
 constexpr uint32_t kShareKeyBytes = 64u * 8u;
 // The fast-kernel preset of a scene's features (fast_instance below) and whether it shares.
 constexpr uint32_t preset_of(uint32_t features) {
@@ -714,10 +721,12 @@ constexpr uint32_t preset_of(uint32_t features) {
            : (features & ~kFRuns) == 0u                          ? kFRuns
            : (features & ~kFBvh) == 0u                           ? kFBvh
            : (features & ~(kFBvh | kFMarble)) == 0u              ? (kFBvh | kFMarble)
-           : (features & ~(kFBvh | kFTri | kFDeep)) == 0u        ? (kFBvh | kFTri | kFDeep | kFSusp)
+           : (features & ~(kFBvh | kFTri | kFDeep)) == 0u        ? (kFBvh | kFTri | kFDeep | (RT_SHARE_TRI ? 0u : kFSusp))
                                                                  : kFAll;
 }
-constexpr bool preset_shares(uint32_t preset) { return RT_SHARE && (preset & kFBvh) != 0u && (preset & kFTri) == 0u; }
+constexpr bool preset_shares(uint32_t preset) {
+    return RT_SHARE && (preset & kFBvh) != 0u && ((preset & kFTri) == 0u || (RT_SHARE_TRI && (preset & kFSusp) == 0u));
+}
 // One leaf (primitive or cube). tmax = closest so far; a hit with t == closest is
 // accepted, so later candidates win ties exactly like hittable.rs:110-116.
 // kTop: a top-level entry's primitive, at a wave-uniform address (ld4c: scalar loads)
@@ -1686,6 +1695,10 @@ RT_DEV bool bvh_run_shared(const DevScene& S, float delta, const f4* wrapper, ui
                 const float dox = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(r.o.x), d));
                 const float doy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(r.o.y), d));
                 const float doz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(r.o.z), d));
+                const float ddx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(r.d.x), d));
+                const float ddy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(r.d.y), d));
+                const float ddz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(r.d.z), d));
+                const float dtime = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(r.time), d));
                 const float dix = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(inv.x), d));
                 const float diy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(inv.y), d));
                 const float diz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(inv.z), d));
@@ -1696,9 +1709,20 @@ RT_DEV bool bvh_run_shared(const DevScene& S, float delta, const f4* wrapper, ui
                 const uint32_t down = __builtin_amdgcn_readlane(owner, d);
                 if (!working && j < take) {
                     const uint32_t lvl = dsp - 1u - j;
-                    const uint32_t node = lds[lvl * 128u + d];
-                    const float key = __uint_as_float(lds[lvl * 128u + 64u + d]);
+                    uint32_t node;
+                    float key;
+                    if (!(kF & kFDeep) || lvl < S.stack_depth) {
+                        node = lds[lvl * 128u + d];
+                        key = __uint_as_float(lds[lvl * 128u + 64u + d]);
+                    } else {  // the donor's entry in its wave's HBM slab (kFDeep: bvh_run's push)
+                        const uint32_t* g = S.stack_spill +
+                                            (((size_t)blockIdx.x * S.spill_depth + (lvl - S.stack_depth)) * 64u + d) * 2u;
+                        node = g[0];
+                        key = __uint_as_float(g[1]);
+                    }
                     r.o = mk(dox, doy, doz);
+                    r.d = mk(ddx, ddy, ddz);
+                    r.time = dtime;
                     inv = mk(dix, diy, diz);
                     tmin = dtmin;
                     tmax_entry = dtmax;
@@ -1771,7 +1795,7 @@ RT_DEV bool bvh_run_shared(const DevScene& S, float delta, const f4* wrapper, ui
                         float c = tmr < cap ? tmr : cap;
                         uint32_t code = 0u;
                         const RayD q = to_d(r);
-                        if (leaf_hit<kF, true>(S, lcode, r, q, tmin, c, code, inv)) {
+                        if (leaf_hit<kF, (kF & kFTri) == 0u>(S, lcode, r, q, tmin, c, code, inv)) {
                             const uint32_t rk = rank + (rtdev::leaf_type(lcode) == rtdev::kLeafCube
                                                             ? rtdev::leaf_index(code) - rtdev::leaf_index(lcode)
                                                             : 0u);
@@ -1820,9 +1844,16 @@ RT_DEV bool bvh_run_shared(const DevScene& S, float delta, const f4* wrapper, ui
             sort2(t0, c0, t2, c2);
             sort2(t1, c1, t3, c3);
             sort2(t1, c1, t2, c2);
-            auto push = [&](uint32_t node, float t) {
-                stk[sp * 128u] = node;
-                stk[sp * 128u + 64u] = __float_as_uint(t);
+            auto push = [&](uint32_t node, float t) {  // (kFDeep: past stack_depth in the HBM slab, as bvh_run)
+                if (!(kF & kFDeep) || sp < S.stack_depth) {
+                    stk[sp * 128u] = node;
+                    stk[sp * 128u + 64u] = __float_as_uint(t);
+                } else {
+                    uint32_t* g = S.stack_spill +
+                                  (((size_t)blockIdx.x * S.spill_depth + (sp - S.stack_depth)) * 64u + lane) * 2u;
+                    g[0] = node;
+                    g[1] = __float_as_uint(t);
+                }
                 sp += 1u;
             };
             bool popnext = true;
@@ -1839,8 +1870,17 @@ RT_DEV bool bvh_run_shared(const DevScene& S, float delta, const f4* wrapper, ui
                 bool found = false;
                 while (sp > 0u) {
                     sp -= 1u;
-                    const uint32_t cand = stk[sp * 128u];
-                    const float tenter = __uint_as_float(stk[sp * 128u + 64u]);
+                    uint32_t cand;
+                    float tenter;
+                    if (!(kF & kFDeep) || sp < S.stack_depth) {
+                        cand = stk[sp * 128u];
+                        tenter = __uint_as_float(stk[sp * 128u + 64u]);
+                    } else {
+                        const uint32_t* g = S.stack_spill +
+                                            (((size_t)blockIdx.x * S.spill_depth + (sp - S.stack_depth)) * 64u + lane) * 2u;
+                        cand = g[0];
+                        tenter = __uint_as_float(g[1]);
+                    }
                     if (!prune || !(tenter > prune_bound(closest))) {
                         cur = cand;
                         found = true;
@@ -2928,6 +2968,9 @@ RT_DEV bool take_sample(ItemPool& pool, bool want, const DevCamera& C, const Dev
                 uint32_t by = blk / P.blocks_x, bx = blk - by * P.blocks_x;
                 x = bx * 8u + (pib & 7u);
                 y = by * 8u + (pib >> 3);
+#ifdef RT_PROFILE_REGIONS
+                if (by < g_prof_rows[0] || by >= g_prof_rows[1]) s = Q.samples;  // outside the profiled band
+#endif
             }
             if (x < P.width && y < P.height && s < Q.samples) {
                 const uint32_t pixel = y * P.width + x;
@@ -3568,7 +3611,8 @@ TraceKernel fast_instance(uint32_t features) {
         case kFRuns: return preset_instance<kWaves, kFRuns>();
         case kFBvh: return preset_instance<kWaves, kFBvh>();
         case kFBvh | kFMarble: return preset_instance<kWaves, kFBvh | kFMarble>();
-        case kFBvh | kFTri | kFDeep | kFSusp: return preset_instance<kWaves, kFBvh | kFTri | kFDeep | kFSusp>();
+        case kFBvh | kFTri | kFDeep | (RT_SHARE_TRI ? 0u : kFSusp):
+            return preset_instance<kWaves, kFBvh | kFTri | kFDeep | (RT_SHARE_TRI ? 0u : kFSusp)>();
         default: return preset_instance<kWaves, kFAll>();
     }
 }
@@ -4493,6 +4537,15 @@ int rt_scene_trace_time(rt_scene_handle s, double* total_ms, uint64_t* launches,
     if (reset) s->ev_count = 0;
     return RT_OK;
 }
+
+#ifdef RT_PROFILE_REGIONS
+// Profiling build only (not in include/rt.h): render only the 8x8-block rows [r0, r1) of later
+// launches (tools/region_profile.py --rows); r1 = ~0u restores the whole frame.
+int rt_prof_rows(uint32_t r0, uint32_t r1) {
+    const uint32_t rows[2] = {r0, r1};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_prof_rows), rows, sizeof rows) == hipSuccess ? RT_OK : RT_ERR_HIP;
+}
+#endif
 
 int rt_device_kat(int op, const float* in, float* out, uint32_t n) {
     rthost::clear_error();

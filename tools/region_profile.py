@@ -36,9 +36,16 @@ def main():
     ap.add_argument("--config", default="C3")
     ap.add_argument("--spp", type=int, default=None)
     ap.add_argument("--shard", type=int, default=1, help="render shard 0 of N (bench.py's block interleave)")
+    ap.add_argument("--rows", default=None,
+                    help="r0:r1 — render only the 8x8-block rows [r0, r1) (rt_prof_rows; the profiling build)")
+    ap.add_argument("--bands", type=int, default=0,
+                    help="profile the frame in this many bands of block rows, one launch each, and print a "
+                         "per-band table (cycles per segment and per-entry shares)")
     args = ap.parse_args()
     if not any(k in os.environ.get("RT_LIBRARY", "") for k in ("_prof", "_audit")):
         sys.exit("set RT_LIBRARY to the _prof or _audit build")
+    if args.bands:
+        return bands(args)
     import torch
     import raytracinginoneweekendinrust_amd as rt
     sys.path.insert(0, os.path.join(ROOT, "tools"))
@@ -48,6 +55,12 @@ def main():
     if args.spp:
         cfg = cfg.scaled(cfg.width, args.spp)
     scene = rt.Scene.generate(cfg.scene, cfg.scene_seed)
+    if args.rows:
+        import ctypes as C
+        from raytracinginoneweekendinrust_amd import _capi
+        r0, r1 = (int(v) for v in args.rows.split(":"))
+        _capi.lib.rt_prof_rows.argtypes = [C.c_uint32, C.c_uint32]
+        assert _capi.lib.rt_prof_rows(r0, r1) == 0
     ds = rt.DeviceScene(scene)
     p = rt.render_params(cfg.width, cfg.height, cfg.spp, cfg.depth, background=cfg.background(), seed=cfg.render_seed,
                          shard_index=0, shard_count=args.shard)
@@ -88,6 +101,48 @@ def main():
     print(f"{'region':34s} {'cyc%':>7s} {'wave-execs':>12s} {'lanes':>6s} {'cyc/exec':>9s}")
     for name, frac, c, ln, ce in rows:
         print(f"{name:34s} {100 * frac:7.2f} {c:12d} {ln:6.1f} {ce:9.0f}")
+    print(json.dumps({"band": args.rows, "trace_ms": ms, "segments": segments, "wave_cycles": total,
+                      "regions": {name: {"cyc": cyc[i], "execs": cnt[i], "lanes": lanes[i]}
+                                  for i, name in enumerate(_names(cfg)) if cnt[i]}}))
+
+
+def _names(cfg):
+    out = []
+    for i in range(COUNT):
+        out.append(EXTRA[i] if i in EXTRA else NAMES[i] if i < ENTRY0 else (
+            f"entry {i - ENTRY0}: " + (SHOWCASE[i - ENTRY0] if cfg.scene == "showcase" and i - ENTRY0 < len(SHOWCASE)
+                                       else "")))
+    return out
+
+
+def bands(args):
+    """One launch per band of 8x8-block rows (a process each: the library's counters accumulate for
+    the process), then per band: wave cycles per segment and the per-region cycles per segment."""
+    import subprocess
+    sys.path.insert(0, ROOT)
+    from raytracinginoneweekendinrust_amd.configs import CONFIGS
+    cfg = CONFIGS[args.config]
+    rows_total = (cfg.height + 7) // 8
+    edges = [round(i * rows_total / args.bands) for i in range(args.bands + 1)]
+    res = []
+    for b in range(args.bands):
+        cmd = [sys.executable, os.path.abspath(__file__), "--config", args.config, "--rows", f"{edges[b]}:{edges[b + 1]}"]
+        if args.spp:
+            cmd += ["--spp", str(args.spp)]
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+        if r.returncode != 0:
+            sys.exit(r.stderr[-2000:])
+        line = [ln for ln in r.stdout.splitlines() if ln.startswith('{"band"')][-1]
+        res.append(json.loads(line))
+        print(r.stdout, flush=True)
+    keys = [k for k in res[0]["regions"] if k.startswith("entry") or k.startswith("BVH") or k in
+            ("Refill", "Record", "Marble", "UnitSphere", "MediumLog", "Scatter")]
+    print(f"{'rows':>9s} {'segs':>11s} {'cyc/seg':>8s} " + " ".join(f"{k[:12]:>12s}" for k in keys))
+    for r in res:
+        segs = max(r["segments"], 1)
+        print(f"{r['band']:>9s} {r['segments']:11d} {r['wave_cycles'] / segs:8.0f} " +
+              " ".join(f"{r['regions'].get(k, {}).get('cyc', 0) / segs:12.0f}" for k in keys))
+    print(json.dumps({"bands": res}))
 
 
 if __name__ == "__main__":

@@ -3,7 +3,7 @@
 # the position-coded gather at world 8), then the whole GPU suite (with the round-6 zero-direction
 # cases on the triangle BVH), then the C3 and C4 bench lines.
 set -u
-cd "$(dirname "$0")/../.."
+cd "$(dirname "$0")/../../.."
 OUT=gpurun_out/r06_s1
 mkdir -p "$OUT"
 export TMPDIR=/tmp
