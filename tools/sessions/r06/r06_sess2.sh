@@ -20,12 +20,12 @@ run() {  # run <log> <seconds> <cmd...>
         exit $rc
     fi
 }
-run parity.log 600 python3 -u -m pytest tests/test_gpu_parity.py -x -v --timeout 300 --timeout-method thread \
-    -k "golden or other_seeds or traversal_audit or pruned_traversal or every_feature or zero_direction or depth_limits or degenerate or full_workload or c1_full"
-run parity_sharetri.log 600 env RT_LIBRARY=raytracinginoneweekendinrust_amd/_lib/librtamd_sharetri.so python3 -u -m pytest tests/test_gpu_parity.py -x -v --timeout 300 --timeout-method thread \
-    -k "c4 or C4 or zero_direction or suspending or every_feature"
 run ab.log 600 bash tools/ab_session.sh r06_share "C3:100 C1" raytracinginoneweekendinrust_amd/_lib/librtamd.so \
     raytracinginoneweekendinrust_amd/_lib/librtamd_noshare.so
 run ab_c4.log 600 bash tools/ab_session.sh r06_sharetri "C4:50" raytracinginoneweekendinrust_amd/_lib/librtamd.so \
     raytracinginoneweekendinrust_amd/_lib/librtamd_sharetri.so
+run parity.log 600 python3 -u -m pytest tests/test_gpu_parity.py -x -v --timeout 300 --timeout-method thread \
+    -k "golden or other_seeds or traversal_audit or pruned_traversal or every_feature or zero_direction or depth_limits or degenerate or full_workload or c1_full"
+run parity_sharetri.log 600 env RT_LIBRARY=raytracinginoneweekendinrust_amd/_lib/librtamd_sharetri.so python3 -u -m pytest tests/test_gpu_parity.py -x -v --timeout 300 --timeout-method thread \
+    -k "c4 or C4 or zero_direction or suspending or every_feature"
 echo "== done" | tee -a "$OUT/session.log"
