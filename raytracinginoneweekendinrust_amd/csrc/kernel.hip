@@ -1657,6 +1657,15 @@ RT_DEV bool bvh_run(const DevScene& S, float delta, const f4* wrapper, const Ray
 // conservative (exact-pruning argument). The hit's code comes from its rank through the BVH's
 // rank -> code table (lower.cpp bvh_emit, S.rank_code). LDS: 64 keys (512 B) behind the stack.
 constexpr unsigned long long kKeyNone = ~0ull;
+#ifndef RT_SHARE_REFRESH
+#define RT_SHARE_REFRESH 1  // (A/B) read the ray's best key back every trip, to prune with it
+#endif
+#ifndef RT_SHARE_MAXWORK
+#define RT_SHARE_MAXWORK 64  // (A/B) hand over only while at most this many lanes traverse
+#endif
+#ifndef RT_SHARE_MINSP
+#define RT_SHARE_MINSP 1  // (A/B) a donor has at least this many pending entries
+#endif
 RT_DEV unsigned long long share_key(float t, uint32_t rank) {
     return ((unsigned long long)__float_as_uint(t) << 32) | (unsigned long long)(~rank);
 }
@@ -1683,8 +1692,8 @@ RT_DEV bool bvh_run_shared(const DevScene& S, float delta, const f4* wrapper, ui
         // (nearest) first; the donor keeps the rest and its current node.
         PROF_T0(psteal);
         const unsigned long long idle = __ballot(!working);
-        if (idle != 0ull) {
-            const unsigned long long donors = __ballot(working && sp > 0u);
+        if (idle != 0ull && (uint32_t)__popcll(idle) >= 64u - RT_SHARE_MAXWORK) {
+            const unsigned long long donors = __ballot(working && sp >= RT_SHARE_MINSP);
             if (donors != 0ull) {
                 const uint32_t d = (uint32_t)__builtin_ctzll(donors);
                 const uint32_t dsp = __builtin_amdgcn_readlane(sp, d);
@@ -1740,7 +1749,7 @@ RT_DEV bool bvh_run_shared(const DevScene& S, float delta, const f4* wrapper, ui
         if (__ballot(working) == 0ull) break;
         if (working) {
             // the best candidate any lane found for this ray so far
-            {
+            if (RT_SHARE_REFRESH) {
                 const unsigned long long kb = keys[owner];
                 if (kb < share_key(closest, best_rank)) {
                     closest = __uint_as_float((uint32_t)(kb >> 32));
