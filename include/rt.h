@@ -85,9 +85,10 @@ typedef enum rt_node_kind {
                                  ref[2] root_index (relative to ref[0]), f[0] / f[1]
                                  ignored (the reference's Bvh stores no shutter times),
                                  f[2] = 1: built
-                                 with Bvh::with_predictor (HRPP only). The device
-                                 traverses this tree as given: its shape and boxes
-                                 decide every box test and every DFS-rank tie. */
+                                 with Bvh::with_predictor (HRPP only). Its boxes and
+                                 leaf nodes decide the visit set and every DFS-rank
+                                 tie, as BvhNode::hit walks the array (the fast kernel
+                                 may rebuild the interior levels: RT_OPT_BVH_SHAPE). */
 } rt_node_kind;
 
 /* One reference BvhNode (src/bvh.rs:228-235), children as the enum Child
@@ -320,6 +321,9 @@ int rt_bvh_build_order(const float* d_keys, uint32_t n, uint64_t seed, uint32_t*
  *                           (default), 1 = host always, 2 = device always
  *   RT_OPT_GUIDE            guided batch divisor K: a batch is at most (units left) /
  *                           (K x waves) units (1..256; 0 = the default 2)
+ *   RT_OPT_BVH_SHAPE        the fast kernel's BVH4 over each BVH's leaf nodes, read at upload:
+ *                           0 = interior levels rebuilt by the surface-area heuristic (default),
+ *                           1 = the reference tree collapsed as built; the same image either way
  * Returns RT_ERR_INVALID for an unknown option or a value out of range. */
 typedef enum {
     RT_OPT_TUNE = 0,
@@ -330,7 +334,8 @@ typedef enum {
     RT_OPT_LAUNCH_LOG = 5,
     RT_OPT_BVH_BUILD = 6,
     RT_OPT_GUIDE = 7,
-    RT_OPT_COUNT = 8
+    RT_OPT_BVH_SHAPE = 8,
+    RT_OPT_COUNT = 9
 } rt_option;
 int rt_set_option(int option, int64_t value);
 int rt_get_option(int option, int64_t* value);

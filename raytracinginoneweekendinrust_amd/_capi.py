@@ -30,7 +30,7 @@ RT_FLAG_FRAMES_IN_FLIGHT = 16
 
 # rt_option (rt_set_option): the library's diagnostic switches; it reads no environment
 OPTIONS = {"tune": 0, "group": 1, "stack_lds": 2, "sample_buffer_mb": 3, "hrpp_slot_bits": 4, "launch_log": 5,
-           "bvh_build": 6, "guide": 7}
+           "bvh_build": 6, "guide": 7, "bvh_shape": 8}
 
 STATUS = {0: "RT_OK", -1: "RT_ERR_INVALID", -2: "RT_ERR_UNSUPPORTED", -3: "RT_ERR_HIP", -4: "RT_ERR_OOM",
           -5: "RT_ERR_NO_DEVICE", -6: "RT_ERR_IO"}

@@ -708,7 +708,7 @@ constexpr uint32_t kFSusp = 64u;
 // per-lane loop for A/B) keeps 64 result keys per wave behind the stack: 9728 + 512 B = 10 KB per
 // wave still fits 16 waves/CU (160 KB).
 #ifndef RT_SHARE
-#define RT_SHARE 1
+#define RT_SHARE 0  // measured slower (C3 100 spp 83.3 -> 90.7 ms, C1 -7%: the denser issue lowered the clock)
 #endif
 // RT_SHARE_TRI (A/B): the triangle preset without the suspending walk, traversing across lanes
 #ifndef RT_SHARE_TRI
@@ -3630,7 +3630,7 @@ TraceKernel fast_instance(int waves, uint32_t features) {
 }
 
 // rt_set_option's process-wide diagnostic switches (include/rt.h rt_option).
-std::atomic<int64_t> g_opt[RT_OPT_COUNT] = {{0}, {0}, {0}, {0}, {-1}, {0}, {0}, {0}};
+std::atomic<int64_t> g_opt[RT_OPT_COUNT] = {{0}, {0}, {0}, {0}, {-1}, {0}, {0}, {0}, {0}};
 int64_t opt(int o) { return g_opt[o].load(std::memory_order_relaxed); }
 
 int check_device(int device) {
@@ -3683,7 +3683,7 @@ int rt_scene_upload(const rt_scene_desc* desc, int device, rt_scene_handle* out)
     rthost::BvhOrderer orderer{16384u, rthost::device_bvh_order, &dev};
     if (mode == 2) orderer.min_items = 1u;
     const bool host_only = mode == 1;
-    int rc = rthost::lower_scene(desc, &hs, &err, host_only ? nullptr : &orderer);
+    int rc = rthost::lower_scene(desc, &hs, &err, host_only ? nullptr : &orderer, (int)opt(RT_OPT_BVH_SHAPE));
     if (rc) return rthost::set_error(rc, err);
     if (hs.max_stack > 96 || hs.max_stack_ref > 96)
         return rthost::set_error(RT_ERR_UNSUPPORTED, "BVH too deep for the LDS traversal stack");
@@ -4508,6 +4508,7 @@ int rt_set_option(int option, int64_t value) {
         case RT_OPT_LAUNCH_LOG: ok = value == 0 || value == 1; break;
         case RT_OPT_BVH_BUILD: ok = value >= 0 && value <= 2; break;
         case RT_OPT_GUIDE: ok = value >= 0 && value <= 256; break;
+        case RT_OPT_BVH_SHAPE: ok = value == 0 || value == 1; break;
     }
     if (!ok) return rthost::set_error(RT_ERR_INVALID, "option value out of range");
     g_opt[option].store(value, std::memory_order_relaxed);

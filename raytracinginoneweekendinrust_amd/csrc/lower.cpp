@@ -233,8 +233,8 @@ struct LeafInfo {
 
 class Lowerer {
    public:
-    Lowerer(const rt_scene_desc* d, HostScene* out, std::string* err, const BvhOrderer* orderer)
-        : d_(d), s_(out), err_(err), orderer_(orderer) {}
+    Lowerer(const rt_scene_desc* d, HostScene* out, std::string* err, const BvhOrderer* orderer, int bvh_shape)
+        : d_(d), s_(out), err_(err), orderer_(orderer), bvh_shape_(bvh_shape) {}
 
     int run() {
         if (!d_ || !d_->nodes || d_->num_nodes == 0) return fail(RT_ERR_INVALID, "empty scene");
@@ -798,37 +798,122 @@ class Lowerer {
             float dx = b.mx.x - b.mn.x, dy = b.mx.y - b.mn.y, dz = b.mx.z - b.mn.z;
             return dx * dy + dy * dz + dz * dx;
         };
+        // The binary tree the BVH4 is collapsed from. The reference tree's leaf nodes (the BvhNodes
+        // whose children are objects: bvh.rs never mixes objects and nodes under one node) are the
+        // units of the fast traversal: a BVH4 leaf node holds one of them and its two objects are
+        // tested exactly as BvhNode::hit tests them (bvh.rs:377-414), after the reference's own
+        // test of that node's box, which the parent slot holds. Which interior nodes lead there does
+        // not change the result: the reference's interior boxes are unions of their children's
+        // (bvh.rs:294-300; prebuilt trees are checked for containment), so a leaf node whose own
+        // box passes the slab test with the BVH's entry t_max has every reference ancestor pass too
+        // (the slab arithmetic is monotone in the box: the BVH4-collapse argument), i.e. it is in
+        // the reference's visit set; and an interior node made of unions of leaf-node boxes passes
+        // whenever one of its leaf nodes does, so no leaf node of the visit set is ever cut off.
+        // Candidates merge by (t, DFS rank) and pruning needs only boxes that contain their
+        // objects. So the interior levels are rebuilt here by the surface-area heuristic over the
+        // leaf nodes (RT_OPT_BVH_SHAPE 0, the default): the reference's median splits on random axes
+        // (bvh.rs:255-257) give boxes that overlap heavily. RT_OPT_BVH_SHAPE 1 collapses the
+        // reference tree as built (rounds 1-5). The reference kernel's BVH2 (nodes2) and the DFS
+        // ranks always come from the reference tree.
+        std::vector<TNode> sah_nodes;  // tn's nodes, then the SAH interior nodes
+        const std::vector<TNode>* T = &tn;
+        uint32_t root2 = troot;
+        if (bvh_shape_ == kBvhShapeSah) {
+            std::vector<uint32_t> units;
+            std::vector<uint32_t> todo{troot};
+            while (!todo.empty()) {
+                const uint32_t i = todo.back();
+                todo.pop_back();
+                if (tn[i].is_node[0] || tn[i].is_node[1]) {
+                    for (int k = 0; k < 2; ++k)
+                        if (tn[i].is_node[k]) todo.push_back(tn[i].child[k]);
+                } else {
+                    units.push_back(i);
+                }
+            }
+            if (units.size() >= 3) {
+                sah_nodes = tn;
+                std::sort(units.begin(), units.end());  // a deterministic start order
+                auto cen = [&](uint32_t u, int a) {
+                    const Box& b = tn[u].box;
+                    return a == 0 ? b.mn.x + b.mx.x : (a == 1 ? b.mn.y + b.mx.y : b.mn.z + b.mx.z);
+                };
+                std::vector<float> right_area;
+                std::function<uint32_t(uint32_t*, uint32_t, uint32_t)> sah = [&](uint32_t* u, uint32_t n,
+                                                                                 uint32_t depth) -> uint32_t {
+                    if (n == 1) return u[0];
+                    int best_axis = -1;
+                    uint32_t best_split = n / 2;
+                    double best_cost = 0.0;
+                    if (depth < 40) {  // (deeper: median splits, so that the tree depth stays bounded)
+                        std::vector<uint32_t> v(u, u + n);
+                        right_area.assign(n, 0.0f);
+                        for (int a = 0; a < 3; ++a) {
+                            std::stable_sort(v.begin(), v.end(), [&](uint32_t p, uint32_t q) { return cen(p, a) < cen(q, a); });
+                            Box acc = tn[v[n - 1]].box;
+                            for (uint32_t i = n - 1; i >= 1; --i) {
+                                acc = box_union(acc, tn[v[i]].box);
+                                right_area[i] = area(acc);
+                            }
+                            acc = tn[v[0]].box;
+                            for (uint32_t i = 1; i < n; ++i) {  // left = v[0, i), right = v[i, n)
+                                const double c = (double)area(acc) * i + (double)right_area[i] * (n - i);
+                                if (best_axis < 0 || c < best_cost) {
+                                    best_cost = c;
+                                    best_axis = a;
+                                    best_split = i;
+                                }
+                                acc = box_union(acc, tn[v[i]].box);
+                            }
+                        }
+                    }
+                    const int a = best_axis < 0 ? 0 : best_axis;
+                    std::stable_sort(u, u + n, [&](uint32_t p, uint32_t q) { return cen(p, a) < cen(q, a); });
+                    const uint32_t l = sah(u, best_split, depth + 1);
+                    const uint32_t r = sah(u + best_split, n - best_split, depth + 1);
+                    TNode t;
+                    t.child[0] = l;
+                    t.child[1] = r;
+                    t.is_node[0] = t.is_node[1] = true;
+                    t.box = box_union(sah_nodes[l].box, sah_nodes[r].box);
+                    t.leaf_box[0] = t.leaf_box[1] = Box{{0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f}};
+                    sah_nodes.push_back(t);
+                    return (uint32_t)sah_nodes.size() - 1;
+                };
+                root2 = sah(units.data(), (uint32_t)units.size(), 1);
+                T = &sah_nodes;
+            }
+        }
+        const std::vector<TNode>& tt = *T;
         std::vector<std::vector<Slot>> wide;  // per wide node, in DFS preorder
-        std::vector<uint32_t> wide_depth;
         std::function<uint32_t(uint32_t, uint32_t)> build4 = [&](uint32_t x, uint32_t depth) -> uint32_t {
             std::vector<Slot> sl;
             for (int k = 0; k < 2; ++k) {
-                if (tn[x].is_node[k]) sl.push_back({true, tn[x].child[k], tn[tn[x].child[k]].box, 0u});
-                else if (tn[x].child[k] != rtdev::kChildEmpty)
-                    sl.push_back({false, tn[x].child[k], tn[x].leaf_box[k], rank[2 * x + k]});
+                if (tt[x].is_node[k]) sl.push_back({true, tt[x].child[k], tt[tt[x].child[k]].box, 0u});
+                else if (tt[x].child[k] != rtdev::kChildEmpty)
+                    sl.push_back({false, tt[x].child[k], tt[x].leaf_box[k], rank[2 * x + k]});
             }
             while (sl.size() < rtdev::kBvhWidth) {
                 int best = -1;
                 for (int k = 0; k < (int)sl.size(); ++k) {
                     if (!sl[k].node) continue;
-                    const TNode& c = tn[sl[k].id];
+                    const TNode& c = tt[sl[k].id];
                     if (!(c.is_node[0] && c.is_node[1])) continue;
                     if (best < 0 || area(sl[k].box) > area(sl[best].box)) best = k;
                 }
                 if (best < 0) break;
-                const TNode c = tn[sl[best].id];
-                sl[best] = {true, c.child[0], tn[c.child[0]].box, 0u};
-                sl.insert(sl.begin() + best + 1, Slot{true, c.child[1], tn[c.child[1]].box, 0u});
+                const TNode c = tt[sl[best].id];
+                sl[best] = {true, c.child[0], tt[c.child[0]].box, 0u};
+                sl.insert(sl.begin() + best + 1, Slot{true, c.child[1], tt[c.child[1]].box, 0u});
             }
             uint32_t me = (uint32_t)wide.size();
             wide.push_back({});
-            wide_depth.push_back(depth);
             for (Slot& c : sl)
                 if (c.node) c.id = build4(c.id, depth + 1) | 0x40000000u;  // mark: wide index (remapped below)
             wide[me] = sl;
             return me;
         };
-        uint32_t wroot = build4(troot, 1);
+        uint32_t wroot = build4(root2, 1);
         // The reference tree itself, as 64 B BVH2 nodes (both children's boxes,
         // child codes), DFS preorder behind a wrapper whose child 0 is the root:
         // traversed in the reference's own recursion order by rays that can take
@@ -941,14 +1026,22 @@ class Lowerer {
                 }
             }
         }
-        uint32_t max_wide_depth = 0;
-        for (uint32_t w = 0; w < wide.size(); ++w) {
-            put(base + 1 + w, wide[w], 0u);
-            max_wide_depth = std::max(max_wide_depth, wide_depth[w]);
+        for (uint32_t w = 0; w < wide.size(); ++w) put(base + 1 + w, wide[w], 0u);
+        // The traversal stack a BVH4 walk needs at most: a visit of an interior node with k children
+        // pushes the k - 1 it does not descend into first (2 words each) and descends into the
+        // nearest, so need(w) = k - 1 + max need(child); a sibling popped later runs with fewer
+        // entries of w beneath it. Wide nodes are in preorder (children after parents). The BVH2
+        // recursion (reference kernel) keeps one 4-word frame per level.
+        std::vector<uint32_t> need(wide.size(), 0u);
+        for (uint32_t w = (uint32_t)wide.size(); w-- > 0;) {
+            uint32_t deepest = 0, k = 0;
+            for (const Slot& c : wide[w]) {
+                ++k;
+                if (c.node) deepest = std::max(deepest, need[c.id & ~0x40000000u]);
+            }
+            need[w] = leaf_node(w) ? 0u : (k - 1u) + deepest;
         }
-        // a BVH4 visit pushes at most kBvhWidth - 1 siblings per level (2 words
-        // each); the BVH2 recursion (reference kernel) keeps one 4-word frame per level
-        s_->max_stack = std::max(s_->max_stack, (rtdev::kBvhWidth - 1u) * max_wide_depth + 1u);
+        s_->max_stack = std::max(s_->max_stack, need.empty() ? 1u : std::max(1u, need[0]));
         s_->max_stack_ref = std::max(s_->max_stack_ref, 2u * (max_depth_ + 2u));
         s_->max_bvh_depth = std::max(s_->max_bvh_depth, max_depth_ + 1);
         *root_out = base;
@@ -1023,6 +1116,7 @@ class Lowerer {
     HostScene* s_;
     std::string* err_;
     const BvhOrderer* orderer_ = nullptr;
+    int bvh_shape_ = kBvhShapeSah;
     std::vector<rtdev::DevEntry> aux_;
     std::unordered_map<int, uint32_t> tex_memo_, mat_memo_, prim_memo_, phase_memo_;
     uint32_t max_depth_ = 0;
@@ -1034,9 +1128,9 @@ class Lowerer {
 
 }  // namespace
 
-int lower_scene(const rt_scene_desc* desc, HostScene* out, std::string* err, const BvhOrderer* orderer) {
+int lower_scene(const rt_scene_desc* desc, HostScene* out, std::string* err, const BvhOrderer* orderer, int bvh_shape) {
     *out = HostScene();
-    Lowerer l(desc, out, err, orderer);
+    Lowerer l(desc, out, err, orderer, bvh_shape);
     int rc = l.run();
     {  // HRPP leaf map sorted by key (binary search on the device)
         std::vector<uint32_t> idx(out->hrpp_keys.size());

@@ -49,8 +49,12 @@ struct BvhOrderer {
     void* ctx;
 };
 
+// The tree shape of the fast kernel's BVH4 (rt.h RT_OPT_BVH_SHAPE): rebuilt by SAH over the reference
+// tree's leaf nodes (0, the default), or the reference tree collapsed as built (1).
+constexpr int kBvhShapeSah = 0, kBvhShapeReference = 1;
 // Returns RT_OK or a negative rt_status with a message in *err.
-int lower_scene(const rt_scene_desc* desc, HostScene* out, std::string* err, const BvhOrderer* orderer = nullptr);
+int lower_scene(const rt_scene_desc* desc, HostScene* out, std::string* err, const BvhOrderer* orderer = nullptr,
+                int bvh_shape = kBvhShapeSah);
 
 // BvhOrderer::fn backed by rt_bvh_build_order on device *(int*)ctx (bvh_build.hip).
 int device_bvh_order(void* ctx, const float* keys, uint32_t n, uint64_t seed, uint32_t* order, std::string* err);

@@ -286,6 +286,20 @@ def _c4_with_spheres(rt):
     return b.finish(w)
 
 
+@pytest.mark.parametrize("cfg_name,width,spp", [("C1", 64, 4), ("C3", 48, 3), ("C4", 40, 2)])
+def test_bvh_shapes_render_the_same_bits(cfg_name, width, spp, rt, orc):
+    # The fast kernel's BVH4 is rebuilt by SAH over the reference tree's leaf nodes (the default,
+    # RT_OPT_BVH_SHAPE 0) or collapsed from the reference tree as built (1): different trees, the
+    # same visit set of leaf nodes and the same (t, DFS rank) winner, so the same bits and segments.
+    cfg, scene, params = setup(rt, cfg_name, width, spp)
+    want, cnt = orc.render(scene, cfg.camera(), params)
+    for shape in (0, 1):
+        with rt.options(bvh_shape=shape):
+            got, st = gpu_render(rt, scene, cfg.camera(), params)
+        np.testing.assert_array_equal(got, want)
+        assert st["segments"] == cnt["segments"]
+
+
 # --- sharding / determinism (the multi-GPU decomposition) ---------------------------
 @pytest.mark.parametrize("n", [2, 3, 8])
 def test_gpu_shards_compose_bit_identically(n, rt):

@@ -6,9 +6,9 @@ import os
 
 ENV = {"RT_TUNE": "tune", "RT_GROUP": "group", "RT_STACK_LDS": "stack_lds", "RT_SAMPLE_BUFFER_MB": "sample_buffer_mb",
        "RT_HRPP_SLOT_BITS": "hrpp_slot_bits", "RT_LAUNCH_LOG": "launch_log", "RT_BVH_BUILD": "bvh_build",
-       "RT_GUIDE": "guide"}
+       "RT_GUIDE": "guide", "RT_BVH_SHAPE": "bvh_shape"}
 OPT_IDS = {"tune": 0, "group": 1, "stack_lds": 2, "sample_buffer_mb": 3, "hrpp_slot_bits": 4, "launch_log": 5,
-           "bvh_build": 6, "guide": 7}
+           "bvh_build": 6, "guide": 7, "bvh_shape": 8}
 
 
 def from_env() -> dict:
