@@ -1227,6 +1227,12 @@ constexpr uint32_t kSuspMinTrips = RT_SUSP_MIN_TRIPS;
 #ifndef RT_LEAF_Q
 #define RT_LEAF_Q 8
 #endif
+#ifndef RT_PUSH_BF
+#define RT_PUSH_BF 0  // (A/B) branch-free pushes of a node's far children (bvh_run)
+#endif
+#ifndef RT_SORT3
+#define RT_SORT3 0  // (A/B) a 4-comparator partial order of the children instead of the 5-comparator sort
+#endif
 template <int kKind, uint32_t kF, bool kSusp>
 RT_DEV bool bvh_run(const DevScene& S, float delta, const f4* wrapper, const Ray& r, V inv, float tmin, float& closest,
                     uint32_t& hit_code, uint32_t* stk, uint32_t mode, Trav& tv, uint32_t susp);
@@ -1565,12 +1571,34 @@ RT_DEV bool bvh_run(const DevScene& S, float delta, const f4* wrapper, const Ray
         sort2(t0, c0, t1, c1);
         sort2(t2, c2, t3, c3);
         sort2(t0, c0, t2, c2);
+#if RT_SORT3
+        // (A/B) the nearest only: t0 is the minimum; t2 (the larger pair minimum) goes on top
+        sort2(t1, c1, t2, c2);  // (t1 <= t2 now; t3 unordered against them)
+#else
         sort2(t1, c1, t3, c3);
         sort2(t1, c1, t2, c2);
+#endif
         if (t0 != kInf) {  // visit the nearest next, push the others far to near
-            if (t3 != kInf) push(c3, t3);
-            if (t2 != kInf) push(c2, t2);
-            if (t1 != kInf) push(c1, t1);
+            if constexpr (RT_PUSH_BF && !(kF & kFDeep)) {
+                // (A/B) branch-free: every entry is written at the top plus the valid ones before it,
+                // so the invalid (t = inf) ones are overwritten or lie past the new top; at most
+                // sp + 2 < the stack bound, since a node with k children is entered with at most
+                // max_stack - (k - 1) entries (lower.cpp's need()).
+                const uint32_t v3 = t3 != kInf ? 1u : 0u, v2 = t2 != kInf ? 1u : 0u, v1 = t1 != kInf ? 1u : 0u;
+                stk[sp * 128u] = c3;
+                stk[sp * 128u + 64u] = __float_as_uint(t3);
+                const uint32_t s2 = sp + v3;
+                stk[s2 * 128u] = c2;
+                stk[s2 * 128u + 64u] = __float_as_uint(t2);
+                const uint32_t s1 = s2 + v2;
+                stk[s1 * 128u] = c1;
+                stk[s1 * 128u + 64u] = __float_as_uint(t1);
+                sp = s1 + v1;
+            } else {
+                if (t3 != kInf) push(c3, t3);
+                if (t2 != kInf) push(c2, t2);
+                if (t1 != kInf) push(c1, t1);
+            }
             cur = c0;
             if constexpr (!kPostpone) {
                 PROF_ADD(kPrBvhPush, pp);
