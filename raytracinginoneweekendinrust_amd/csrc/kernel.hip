@@ -1259,13 +1259,19 @@ RT_DEV bool bvh_run(const DevScene& S, float delta, const f4* wrapper, const Ray
 // direction; a NaN closest_so_far, e.g. from a 0/0 rect hit earlier in the list whose plane axis
 // the BVH's own frame rotated away).
 constexpr uint32_t kRayFast = 0u, kRayHandOver = 1u, kRayNoHit = 2u;
+#ifndef RT_TRI_ZERO_DIR
+#define RT_TRI_ZERO_DIR 1  // (A/B) triangle-only BVHs take zero-direction rays on the fast path
+#endif
+#ifndef RT_TNUM
+#define RT_TNUM 1  // (A/B) the NaN closest_so_far hand-over
+#endif
 template <uint32_t kF>
 RT_DEV uint32_t ray_route(const Ray& r, V inv, float tmax_entry, const f4* wrapper, uint32_t mode) {
     const float ax = __builtin_fabsf(inv.x), ay = __builtin_fabsf(inv.y), az = __builtin_fabsf(inv.z);
     const bool ofin = __builtin_fabsf(r.o.x) < kInf && __builtin_fabsf(r.o.y) < kInf && __builtin_fabsf(r.o.z) < kInf;
-    const bool tnum = tmax_entry == tmax_entry;
+    const bool tnum = !RT_TNUM || tmax_entry == tmax_entry;
     if (ax > 0.0f && ax < kInf && ay > 0.0f && ay < kInf && az > 0.0f && az < kInf && ofin && tnum) return kRayFast;
-    if constexpr ((kF & kFTri) != 0u) {
+    if constexpr ((kF & kFTri) != 0u && RT_TRI_ZERO_DIR) {
         if ((__float_as_uint(ld4c(wrapper + 7).w) & rtdev::kBvhTriOnly) != 0u &&
             !(kPruneAllExpBuild && (mode & kModePruneAllExp))) {
             if (r.o.x != r.o.x || r.o.y != r.o.y || r.o.z != r.o.z || r.d.x != r.d.x || r.d.y != r.d.y ||
