@@ -136,9 +136,9 @@ __device__ unsigned long long g_tp_hist[kTpBuckets];
 constexpr uint32_t kRoleEvents = 4096;
 __device__ unsigned long long g_role_ev[2 * kRoleEvents];
 __device__ unsigned g_role_n;
-// block-row band [g_prof_rows[0], g_prof_rows[1]) the profiling build renders (rt_prof_rows; the
-// other units are claimed and skipped): the region profile of one band of the image
-__device__ uint32_t g_prof_rows[2] = {0u, 0xffffffffu};
+// block-row band [g_prof_rows[0], g_prof_rows[1]) the profiling build renders (rt_prof_rows): the
+// launch's pool holds only that band's blocks (rt_render_launch_camera offsets the block map)
+uint32_t g_prof_rows[2] = {0u, 0xffffffffu};
 __device__ __forceinline__ void role_event(uint32_t what) {
     const unsigned i = atomicAdd(&g_role_n, 1u);
     if (i < kRoleEvents) {
@@ -1227,12 +1227,7 @@ constexpr uint32_t kSuspMinTrips = RT_SUSP_MIN_TRIPS;
 #ifndef RT_LEAF_Q
 #define RT_LEAF_Q 8
 #endif
-#ifndef RT_PUSH_BF
-#define RT_PUSH_BF 0  // (A/B) branch-free pushes of a node's far children (bvh_run)
-#endif
-#ifndef RT_SORT3
-#define RT_SORT3 0  // (A/B) a 4-comparator partial order of the children instead of the 5-comparator sort
-#endif
+
 template <int kKind, uint32_t kF, bool kSusp>
 RT_DEV bool bvh_run(const DevScene& S, float delta, const f4* wrapper, const Ray& r, V inv, float tmin, float& closest,
                     uint32_t& hit_code, uint32_t* stk, uint32_t mode, Trav& tv, uint32_t susp);
@@ -1259,19 +1254,19 @@ RT_DEV bool bvh_run(const DevScene& S, float delta, const f4* wrapper, const Ray
 // direction; a NaN closest_so_far, e.g. from a 0/0 rect hit earlier in the list whose plane axis
 // the BVH's own frame rotated away).
 constexpr uint32_t kRayFast = 0u, kRayHandOver = 1u, kRayNoHit = 2u;
-#ifndef RT_TRI_ZERO_DIR
-#define RT_TRI_ZERO_DIR 1  // (A/B) triangle-only BVHs take zero-direction rays on the fast path
-#endif
-#ifndef RT_TNUM
-#define RT_TNUM 1  // (A/B) the NaN closest_so_far hand-over
-#endif
-template <uint32_t kF>
+// Where: the relaxed rule for triangle-only BVHs is compiled into the replay pass (kKind 3) only,
+// which re-traces the handed-over samples from their camera ray: their zero-direction rays then
+// take its fast traversal instead of the literal recursion over the unpruned mesh (C4's replay
+// tail). In the fast kernel the same code cost the triangle preset's register allocation 10% (C4
+// 50 spp 62.0 vs 68.8 ms, profiles/r06/experiments/ray_route_ab_c4.log) for a few hundred samples
+// per frame, so it hands those over as before.
+template <int kKind, uint32_t kF>
 RT_DEV uint32_t ray_route(const Ray& r, V inv, float tmax_entry, const f4* wrapper, uint32_t mode) {
     const float ax = __builtin_fabsf(inv.x), ay = __builtin_fabsf(inv.y), az = __builtin_fabsf(inv.z);
     const bool ofin = __builtin_fabsf(r.o.x) < kInf && __builtin_fabsf(r.o.y) < kInf && __builtin_fabsf(r.o.z) < kInf;
-    const bool tnum = !RT_TNUM || tmax_entry == tmax_entry;
+    const bool tnum = tmax_entry == tmax_entry;
     if (ax > 0.0f && ax < kInf && ay > 0.0f && ay < kInf && az > 0.0f && az < kInf && ofin && tnum) return kRayFast;
-    if constexpr ((kF & kFTri) != 0u && RT_TRI_ZERO_DIR) {
+    if constexpr ((kF & kFTri) != 0u && kKind == 3) {
         if ((__float_as_uint(ld4c(wrapper + 7).w) & rtdev::kBvhTriOnly) != 0u &&
             !(kPruneAllExpBuild && (mode & kModePruneAllExp))) {
             if (r.o.x != r.o.x || r.o.y != r.o.y || r.o.z != r.o.z || r.d.x != r.d.x || r.d.y != r.d.y ||
@@ -1316,7 +1311,7 @@ RT_DEV bool bvh_hit(const DevScene& S, float delta, uint32_t root, const Ray& r,
     // handed over too: a NaN rect hit leaves a NaN origin for the next bounce, which the replay
     // pass can meet after a bounce the fast kernel never traced. The reference kernel takes them.
     {
-        const uint32_t route = ray_route<kF>(r, inv, closest, wrapper, mode);
+        const uint32_t route = ray_route<kKind, kF>(r, inv, closest, wrapper, mode);
         if (route == kRayNoHit) return false;
         if constexpr (kKind == 3) {
             if (route == kRayHandOver)
@@ -1577,34 +1572,12 @@ RT_DEV bool bvh_run(const DevScene& S, float delta, const f4* wrapper, const Ray
         sort2(t0, c0, t1, c1);
         sort2(t2, c2, t3, c3);
         sort2(t0, c0, t2, c2);
-#if RT_SORT3
-        // (A/B) the nearest only: t0 is the minimum; t2 (the larger pair minimum) goes on top
-        sort2(t1, c1, t2, c2);  // (t1 <= t2 now; t3 unordered against them)
-#else
         sort2(t1, c1, t3, c3);
         sort2(t1, c1, t2, c2);
-#endif
         if (t0 != kInf) {  // visit the nearest next, push the others far to near
-            if constexpr (RT_PUSH_BF && !(kF & kFDeep)) {
-                // (A/B) branch-free: every entry is written at the top plus the valid ones before it,
-                // so the invalid (t = inf) ones are overwritten or lie past the new top; at most
-                // sp + 2 < the stack bound, since a node with k children is entered with at most
-                // max_stack - (k - 1) entries (lower.cpp's need()).
-                const uint32_t v3 = t3 != kInf ? 1u : 0u, v2 = t2 != kInf ? 1u : 0u, v1 = t1 != kInf ? 1u : 0u;
-                stk[sp * 128u] = c3;
-                stk[sp * 128u + 64u] = __float_as_uint(t3);
-                const uint32_t s2 = sp + v3;
-                stk[s2 * 128u] = c2;
-                stk[s2 * 128u + 64u] = __float_as_uint(t2);
-                const uint32_t s1 = s2 + v2;
-                stk[s1 * 128u] = c1;
-                stk[s1 * 128u + 64u] = __float_as_uint(t1);
-                sp = s1 + v1;
-            } else {
-                if (t3 != kInf) push(c3, t3);
-                if (t2 != kInf) push(c2, t2);
-                if (t1 != kInf) push(c1, t1);
-            }
+            if (t3 != kInf) push(c3, t3);
+            if (t2 != kInf) push(c2, t2);
+            if (t1 != kInf) push(c1, t1);
             cur = c0;
             if constexpr (!kPostpone) {
                 PROF_ADD(kPrBvhPush, pp);
@@ -2785,14 +2758,9 @@ RT_DEV void world_walk(const DevScene& S, float delta, const Ray& ray, Rng& g, c
             const f4* wrapper = S.nodes + (size_t)root * rtdev::kBvhNodeF4;
             const V inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
             if (!w.resume) {  // bvh_hit's hand-over rule (NaN-prone rays go to the reference kernel)
-                const uint32_t route = ray_route<kF>(r, inv, w.closest, wrapper, mode);
-                if (route == kRayHandOver) {
+                if (ray_route<0, kF>(r, inv, w.closest, wrapper, mode) != kRayFast) {
                     replay = true;
                     w.pos = S.num_top + 1u;  // abandoned: the sample is re-traced by the reference kernel
-                    continue;
-                }
-                if (route == kRayNoHit) {  // a triangle-only BVH takes no NaN ray: no hit, next entry
-                    w.pos = e + 1u;
                     continue;
                 }
                 w.tv = Trav{root, 0u, 0u, w.closest, false, kNoNode};
@@ -3011,9 +2979,6 @@ RT_DEV bool take_sample(ItemPool& pool, bool want, const DevCamera& C, const Dev
                 uint32_t by = blk / P.blocks_x, bx = blk - by * P.blocks_x;
                 x = bx * 8u + (pib & 7u);
                 y = by * 8u + (pib >> 3);
-#ifdef RT_PROFILE_REGIONS
-                if (by < g_prof_rows[0] || by >= g_prof_rows[1]) s = Q.samples;  // outside the profiled band
-#endif
             }
             if (x < P.width && y < P.height && s < Q.samples) {
                 const uint32_t pixel = y * P.width + x;
@@ -4094,6 +4059,14 @@ int rt_render_launch_camera(rt_scene_handle s, const rt_camera* camera, const rt
         if (!(dp.prune_delta < 1e30f)) dp.flags |= RT_FLAG_EXACT_BVH;  // non-finite scene: no pruning
     }
     uint32_t nblk = dp.num_blocks > dp.shard_index ? (dp.num_blocks - dp.shard_index + dp.shard_count - 1u) / dp.shard_count : 0u;
+#ifdef RT_PROFILE_REGIONS
+    if (g_prof_rows[1] != 0xffffffffu && dp.shard_count == 1u) {  // rt_prof_rows: the band's blocks only
+        const uint32_t rows = (dp.height + 7u) / 8u;
+        const uint32_t r0 = std::min(g_prof_rows[0], rows), r1 = std::min(std::max(g_prof_rows[1], r0), rows);
+        dp.shard_index = r0 * dp.blocks_x;  // block = shard_index + local block (shard_count 1)
+        nblk = (r1 - r0) * dp.blocks_x;
+    }
+#endif
     if (nblk == 0) return RT_OK;
     DeviceGuard g(s->device);
     if (!g.ok) return rthost::set_error(RT_ERR_HIP, "hipSetDevice failed");
@@ -4586,8 +4559,9 @@ int rt_scene_trace_time(rt_scene_handle s, double* total_ms, uint64_t* launches,
 // Profiling build only (not in include/rt.h): render only the 8x8-block rows [r0, r1) of later
 // launches (tools/region_profile.py --rows); r1 = ~0u restores the whole frame.
 int rt_prof_rows(uint32_t r0, uint32_t r1) {
-    const uint32_t rows[2] = {r0, r1};
-    return hipMemcpyToSymbol(HIP_SYMBOL(g_prof_rows), rows, sizeof rows) == hipSuccess ? RT_OK : RT_ERR_HIP;
+    g_prof_rows[0] = r0;
+    g_prof_rows[1] = r1;
+    return RT_OK;
 }
 #endif
 
