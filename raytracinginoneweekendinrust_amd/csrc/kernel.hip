@@ -2835,6 +2835,23 @@ RT_DEV ReplayItem replay_take(const ReplayItem* list, uint32_t idx) {
     return ReplayItem{(uint32_t)v, (uint32_t)(v >> 32)};
 }
 constexpr uint32_t kReplayCap = 1u << 20;
+// A finished sample's radiance into the sample buffer (read once, by resolve_samples). RT_SBUF_NT
+// (A/B): non-temporal stores, so the 5.76 GB a C3 frame streams through do not evict the hot lines
+// (scene rows, register spills) from L2.
+#ifndef RT_SBUF_NT
+#define RT_SBUF_NT 0
+#endif
+RT_DEV void sbuf_store(float* o, V L) {
+    if constexpr (RT_SBUF_NT) {
+        __builtin_nontemporal_store(L.x, o);
+        __builtin_nontemporal_store(L.y, o + 1);
+        __builtin_nontemporal_store(L.z, o + 2);
+    } else {
+        o[0] = L.x;
+        o[1] = L.y;
+        o[2] = L.z;
+    }
+}
 // The streaming replay pass (trace_samples<3> with fixup 2, on a second stream) claims
 // entries one at a time while the fast kernel drains. Returns the claimed entry's index once
 // it is published, or kReplayNone when the fast kernel finished without one, the list
@@ -2989,8 +3006,7 @@ RT_DEV bool take_sample(ItemPool& pool, bool want, const DevCamera& C, const Dev
                 depth = P.max_depth;
                 start_sample(C, P, k, x, y, pixel, Q.sample0 + s, g, ray);
                 if (depth == 0u) {
-                    float* o = sbuf + ((size_t)s_local * Q.nslots + sl) * 3u;
-                    o[0] = o[1] = o[2] = 0.0f;
+                    sbuf_store(sbuf + ((size_t)s_local * Q.nslots + sl) * 3u, mk(0.0f, 0.0f, 0.0f));
                 } else {
                     got = true;
                 }
@@ -3051,10 +3067,7 @@ RT_DEV bool finish_segment(const DevScene& S, const DevParams& P, const ChunkPar
         }
     }
     if (done) {
-        float* o = sbuf + ((size_t)s_local * Q.nslots + slot) * 3u;
-        o[0] = L.x;
-        o[1] = L.y;
-        o[2] = L.z;
+        sbuf_store(sbuf + ((size_t)s_local * Q.nslots + slot) * 3u, L);
     }
     PROF_ADD(kPrSegment, pg);
     return done;
@@ -3119,10 +3132,7 @@ RT_DEV bool shade_marble(const DevScene& S, const DevParams& P, const ChunkParam
         else if (scattered) T = T * mk(sv, sv, sv);
     }
     if (shade && done) {
-        float* o = sbuf + ((size_t)s_local * Q.nslots + slot) * 3u;
-        o[0] = L.x;
-        o[1] = L.y;
-        o[2] = L.z;
+        sbuf_store(sbuf + ((size_t)s_local * Q.nslots + slot) * 3u, L);
     }
     return shade && done;
 }
