@@ -118,7 +118,9 @@ static_assert(sizeof(DevTexture) == 32, "DevTexture layout");
 //          (max.x[4]) (max.y[4]) (max.z[4]) (child[4]) (rank[4]); child = node
 //          index (| kLeafNodeFlag for a leaf node), leaf code or kChildEmpty; a leaf slot's box is the leaf's own
 //          bounding box (used only by the conservative leaf reject), its rank the
-//          leaf's DFS ordinal in the reference BVH2. Each BVH starts with a wrapper
+//          leaf's DFS ordinal in the reference BVH2. A leaf node's spheres are repeated
+//          in the free lanes 2 / 3 of rows 0, 1, 2, 6 (lower.cpp bvh_emit put).
+//          Each BVH starts with a wrapper
 //          node whose slot 0 is the root; the wrapper's rank[3] holds kBvhPrunable
 //          when every leaf is a Sphere/Rect/Cube, its rank[2] the BVH2 wrapper.
 //   node2: 64 B reference BVH2 node: (Lmin, Lmax.x) (Lmax.yz, Rmin.xy) (Rmin.z,

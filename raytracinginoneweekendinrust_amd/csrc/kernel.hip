@@ -273,10 +273,15 @@ RT_DEV f4 ld4(const f4* p) {
     return v;
 }
 // Row loads at a 32-bit byte offset from a wave-uniform base (BVH4 nodes: 16-byte rows; the
-// .xy halves of leaf rows at 8-byte granularity).
+// .xy halves of leaf rows at 8-byte granularity; single lanes of leaf rows).
 RT_DEV f4 ld4_at(const f4* base, uint32_t byte_off) {
     f4 v;
     __builtin_memcpy(&v, __builtin_assume_aligned(reinterpret_cast<const char*>(base) + byte_off, 16), sizeof(v));
+    return v;
+}
+RT_DEV float ld1_at(const f4* base, uint32_t byte_off) {
+    float v;
+    __builtin_memcpy(&v, __builtin_assume_aligned(reinterpret_cast<const char*>(base) + byte_off, 4), sizeof(v));
     return v;
 }
 RT_DEV float2 ld2_at(const f4* base, uint32_t byte_off) {
@@ -735,12 +740,52 @@ RT_DEV f4 ldt(const f4* p) {
     if constexpr (kC) return ld4c(p);
     return ld4(p);
 }
-template <uint32_t kF = kFAll, bool kInv = false, bool kTop = false>
+// RT_LEAF_EMBED: the BVH leaf test reads a leaf node's spheres (cx, cy, cz, r; lower.cpp put
+// repeats them in the free slot lanes) and its cubes' bounds (a cube's leaf box is exactly its
+// bounds) from the node's own rows, so it no longer waits on a second, dependent load from sph /
+// rect, nor holds those scene pointers across the traversal loop. 0 builds the round-5 leaf
+// reads (A/B).
+// The sphere-BVH presets only: the triangle preset's instance spilled 10 more VGPRs for code its
+// scenes do not run.
+#ifndef RT_LEAF_EMBED
+#define RT_LEAF_EMBED 1
+#endif
+template <uint32_t kF>
+constexpr bool kLeafEmbed = RT_LEAF_EMBED && (kF & kFTri) == 0u;
+// cube.rs:84-93: the six sides as a HittableList. The sides' axes are fixed (cube.rs:25-74:
+// xy z0, xy z1, xz y0, xz y1, yz x0, yz x1) and their bounds are the box's six values.
+template <bool kInv>
+RT_DEV bool cube_hit(const DevScene& S, uint32_t idx, float x0, float y0, float z0, float x1, float y1, float z1,
+                     const Ray& r, V inv, float tmin, float& closest, uint32_t& hit_code) {
+    const float ox = r.o.x, oy = r.o.y, oz = r.o.z, dx = r.d.x, dy = r.d.y, dz = r.d.z;
+    float t;
+    bool any = false;
+    uint32_t face = 0u;
+    if (kInv && RT_MARKSTEIN_CUBE && S.rect_rcp_ok && rcp_ray_ok(r)) {  // the ray's reciprocals (side_t_rcp)
+        if (side_t_rcp(z0, oz, dz, inv.z, ox, dx, oy, dy, x0, x1, y0, y1, tmin, closest, t)) { closest = t; face = 0u; any = true; }
+        if (side_t_rcp(z1, oz, dz, inv.z, ox, dx, oy, dy, x0, x1, y0, y1, tmin, closest, t)) { closest = t; face = 1u; any = true; }
+        if (side_t_rcp(y0, oy, dy, inv.y, ox, dx, oz, dz, x0, x1, z0, z1, tmin, closest, t)) { closest = t; face = 2u; any = true; }
+        if (side_t_rcp(y1, oy, dy, inv.y, ox, dx, oz, dz, x0, x1, z0, z1, tmin, closest, t)) { closest = t; face = 3u; any = true; }
+        if (side_t_rcp(x0, ox, dx, inv.x, oy, dy, oz, dz, y0, y1, z0, z1, tmin, closest, t)) { closest = t; face = 4u; any = true; }
+        if (side_t_rcp(x1, ox, dx, inv.x, oy, dy, oz, dz, y0, y1, z0, z1, tmin, closest, t)) { closest = t; face = 5u; any = true; }
+    } else {
+        if (side_t(z0, oz, dz, ox, dx, oy, dy, x0, x1, y0, y1, tmin, closest, t)) { closest = t; face = 0u; any = true; }
+        if (side_t(z1, oz, dz, ox, dx, oy, dy, x0, x1, y0, y1, tmin, closest, t)) { closest = t; face = 1u; any = true; }
+        if (side_t(y0, oy, dy, ox, dx, oz, dz, x0, x1, z0, z1, tmin, closest, t)) { closest = t; face = 2u; any = true; }
+        if (side_t(y1, oy, dy, ox, dx, oz, dz, x0, x1, z0, z1, tmin, closest, t)) { closest = t; face = 3u; any = true; }
+        if (side_t(x0, ox, dx, oy, dy, oz, dz, y0, y1, z0, z1, tmin, closest, t)) { closest = t; face = 4u; any = true; }
+        if (side_t(x1, ox, dx, oy, dy, oz, dz, y0, y1, z0, z1, tmin, closest, t)) { closest = t; face = 5u; any = true; }
+    }
+    if (any) hit_code = rtdev::leaf_code(rtdev::kLeafRect, idx + face);
+    return any;
+}
+// kNoSphCube: the caller has tested sphere and cube leaves itself (bvh_run, RT_LEAF_EMBED).
+template <uint32_t kF = kFAll, bool kInv = false, bool kTop = false, bool kNoSphCube = false>
 RT_DEV bool leaf_hit(const DevScene& S, uint32_t code, const Ray& r, const RayD& q, float tmin, float& closest,
                      uint32_t& hit_code, V inv = V{0.0f, 0.0f, 0.0f}) {
     uint32_t type = rtdev::leaf_type(code), idx = rtdev::leaf_index(code);
     float t;
-    if (type == rtdev::kLeafSphere) {
+    if (!kNoSphCube && type == rtdev::kLeafSphere) {
         if (sphere_t(ldt<kTop>(S.sph + idx), q, tmin, closest, t)) {
             closest = t;
             hit_code = code;
@@ -756,33 +801,11 @@ RT_DEV bool leaf_hit(const DevScene& S, uint32_t code, const Ray& r, const RayD&
         }
         return false;
     }
-    if (type == rtdev::kLeafCube) {  // cube.rs:84-93: the six sides as a HittableList
-        // The sides' axes are fixed (cube.rs:25-74: xy z0, xy z1, xz y0, xz y1,
-        // yz x0, yz x1) and their bounds are the box's six values, read from the
-        // records of sides 0 and 2: (z0, x0, x1, y0), y1 and (y0, x0, x1, z0), z1.
+    if (!kNoSphCube && type == rtdev::kLeafCube) {
+        // the bounds from the records of sides 0 and 2: (z0, x0, x1, y0), y1 and (y0, x0, x1, z0), z1
         const f4 s0 = ldt<kTop>(S.rect + 2 * idx);
         const float y1 = ldt<kTop>(S.rect + 2 * idx + 1).x, z1 = ldt<kTop>(S.rect + 2 * idx + 5).x;
-        const float x0 = s0.y, x1 = s0.z, y0 = s0.w, z0 = s0.x;
-        const float ox = r.o.x, oy = r.o.y, oz = r.o.z, dx = r.d.x, dy = r.d.y, dz = r.d.z;
-        bool any = false;
-        uint32_t face = 0u;
-        if (kInv && RT_MARKSTEIN_CUBE && S.rect_rcp_ok && rcp_ray_ok(r)) {  // the ray's reciprocals (side_t_rcp)
-            if (side_t_rcp(z0, oz, dz, inv.z, ox, dx, oy, dy, x0, x1, y0, y1, tmin, closest, t)) { closest = t; face = 0u; any = true; }
-            if (side_t_rcp(z1, oz, dz, inv.z, ox, dx, oy, dy, x0, x1, y0, y1, tmin, closest, t)) { closest = t; face = 1u; any = true; }
-            if (side_t_rcp(y0, oy, dy, inv.y, ox, dx, oz, dz, x0, x1, z0, z1, tmin, closest, t)) { closest = t; face = 2u; any = true; }
-            if (side_t_rcp(y1, oy, dy, inv.y, ox, dx, oz, dz, x0, x1, z0, z1, tmin, closest, t)) { closest = t; face = 3u; any = true; }
-            if (side_t_rcp(x0, ox, dx, inv.x, oy, dy, oz, dz, y0, y1, z0, z1, tmin, closest, t)) { closest = t; face = 4u; any = true; }
-            if (side_t_rcp(x1, ox, dx, inv.x, oy, dy, oz, dz, y0, y1, z0, z1, tmin, closest, t)) { closest = t; face = 5u; any = true; }
-        } else {
-            if (side_t(z0, oz, dz, ox, dx, oy, dy, x0, x1, y0, y1, tmin, closest, t)) { closest = t; face = 0u; any = true; }
-            if (side_t(z1, oz, dz, ox, dx, oy, dy, x0, x1, y0, y1, tmin, closest, t)) { closest = t; face = 1u; any = true; }
-            if (side_t(y0, oy, dy, ox, dx, oz, dz, x0, x1, z0, z1, tmin, closest, t)) { closest = t; face = 2u; any = true; }
-            if (side_t(y1, oy, dy, ox, dx, oz, dz, x0, x1, z0, z1, tmin, closest, t)) { closest = t; face = 3u; any = true; }
-            if (side_t(x0, ox, dx, oy, dy, oz, dz, y0, y1, z0, z1, tmin, closest, t)) { closest = t; face = 4u; any = true; }
-            if (side_t(x1, ox, dx, oy, dy, oz, dz, y0, y1, z0, z1, tmin, closest, t)) { closest = t; face = 5u; any = true; }
-        }
-        if (any) hit_code = rtdev::leaf_code(rtdev::kLeafRect, idx + face);
-        return any;
+        return cube_hit<kInv>(S, idx, s0.y, s0.w, s0.x, s0.z, y1, z1, r, inv, tmin, closest, hit_code);
     }
     if ((kF & kFTri) && type == rtdev::kLeafTri) {
         if (tri_t(ldt<kTop>(S.tri + 3 * idx), ldt<kTop>(S.tri + 3 * idx + 1), ldt<kTop>(S.tri + 3 * idx + 2), r, tmin, closest, t)) {
@@ -1286,6 +1309,12 @@ RT_DEV bool bvh_run_shared(const DevScene& S, float delta, const f4* wrapper, ui
                            uint32_t mode);
 template <uint32_t kF>
 constexpr bool kShare = preset_shares(kF);
+// RT_PEEL_WRAPPER: bvh_hit tests the wrapper's slot (the root box) before the traversal loop (0:
+// the loop's first trip does, A/B).
+#ifndef RT_PEEL_WRAPPER
+#define RT_PEEL_WRAPPER 1
+#endif
+constexpr bool kPeelWrapper = RT_PEEL_WRAPPER;
 // kTop: a top-level entry of the list walk (t_min = 0.001), where the sphere-BVH presets traverse
 // across lanes (bvh_run_shared); medium boundaries (t_min = -inf or t1 + 1e-4) keep bvh_run.
 template <int kKind, uint32_t kF = kFAll, bool kTop = false>
@@ -1327,6 +1356,30 @@ RT_DEV bool bvh_hit(const DevScene& S, float delta, uint32_t root, const Ray& r,
     Trav tv{root, 0u, 0u, closest, false, kNoNode};
     if constexpr (kKind == 0 && kTop && kShare<kF>) {
         tv.any = bvh_run_shared<kF>(S, delta, wrapper, root, r, inv, tmin, closest, hit_code, stk, mode);
+    } else if constexpr (kPeelWrapper) {
+        // The wrapper's one slot (the root's box, bvh.rs:370) tested outside the loop, from scalar
+        // loads at the wave-uniform wrapper address: the loop's first trip, which loads the same
+        // rows for every lane with vector loads, sorts four keys of which three are empty and
+        // pushes nothing, becomes a handful of VALU operations, and a lane whose ray misses the
+        // root box never enters the loop. The same interval, prune bound and result as
+        // child_keys4_nf's slot 0 (see there; no NaN slab value under ray_route), then cur = the
+        // root, with nothing on the stack: the state the loop's first trip leaves.
+        const f4 w0 = ld4c(wrapper), w1 = ld4c(wrapper + 1), w2 = ld4c(wrapper + 2), w3 = ld4c(wrapper + 3),
+                 w4 = ld4c(wrapper + 4), w5 = ld4c(wrapper + 5), w6 = ld4c(wrapper + 6), w7 = ld4c(wrapper + 7);
+        const bool prune = (__float_as_uint(w7.w) & rtdev::kBvhPrunable) != 0u ||
+                           (kPruneAllExpBuild && (mode & kModePruneAllExp));
+        const float dmi = delta * fmaxf(fmaxf(__builtin_fabsf(inv.x), __builtin_fabsf(inv.y)), __builtin_fabsf(inv.z));
+        const bool sx = inv.x < 0.0f, sy = inv.y < 0.0f, sz = inv.z < 0.0f;
+        const float tnx = ((sx ? w3.x : w0.x) - r.o.x) * inv.x, tfx = ((sx ? w0.x : w3.x) - r.o.x) * inv.x;
+        const float tny = ((sy ? w4.x : w1.x) - r.o.y) * inv.y, tfy = ((sy ? w1.x : w4.x) - r.o.y) * inv.y;
+        const float tnz = ((sz ? w5.x : w2.x) - r.o.z) * inv.z, tfz = ((sz ? w2.x : w5.x) - r.o.z) * inv.z;
+        const float lo = __builtin_fmaxf(__builtin_fmaxf(tnx, tny), __builtin_fmaxf(tnz, tmin));
+        const float hi = __builtin_fminf(__builtin_fminf(tfx, tfy), __builtin_fminf(tfz, closest));
+        const float te = lo - (prune ? dmi : 0.0f);
+        if (lo <= hi && te <= (prune ? prune_bound(closest) : kInf)) {
+            tv.cur = __float_as_uint(w6.x);
+            bvh_run<kKind, kF, false>(S, delta, wrapper, r, inv, tmin, closest, hit_code, stk, mode, tv, 0u);
+        }
     } else {
         bvh_run<kKind, kF, false>(S, delta, wrapper, r, inv, tmin, closest, hit_code, stk, mode, tv, 0u);
     }
@@ -1496,7 +1549,31 @@ RT_DEV bool bvh_run(const DevScene& S, float delta, const f4* wrapper, const Ray
                            if (leaf_hit<kF>(S, lcode, r, q, tmin, c2, h2) && h2 == 0x7fffffffu) c = -1.0f;);
                     // cube sides from the ray's reciprocals (side_t_rcp) except in the triangle preset,
                     // whose instance lost 1.6% to the extra code (C3 +2%; uniform_entries_ab.log)
-                    if (leaf_hit<kF, (kF & kFTri) == 0u>(S, lcode, r, q, tmin, c, code, inv)) {
+                    bool hit;
+                    if constexpr (kLeafEmbed<kF>) {
+                        const uint32_t ltype = rtdev::leaf_type(lcode);
+                        // leaf k's lane of rows 0-6 (the node's line, just fetched; the address needs
+                        // no record index, so the loads do not wait on the child row)
+                        const uint32_t lo = nbo + 4u * k;
+                        if (ltype == rtdev::kLeafSphere) {  // (cx, cy, cz, r) in lane 2 + k of rows 0, 1, 2, 6
+                            const f4 sp{ld1_at(nd, lo + 8u), ld1_at(nd, lo + 24u), ld1_at(nd, lo + 40u), ld1_at(nd, lo + 104u)};
+                            float ts;
+                            hit = sphere_t(sp, q, tmin, c, ts);
+                            if (hit) {
+                                c = ts;
+                                code = lcode;
+                            }
+                        } else if (ltype == rtdev::kLeafCube) {  // its leaf box (lane k of rows 0-5) is its bounds
+                            hit = cube_hit<(kF & kFTri) == 0u>(S, rtdev::leaf_index(lcode), ld1_at(nd, lo), ld1_at(nd, lo + 16u),
+                                                               ld1_at(nd, lo + 32u), ld1_at(nd, lo + 48u), ld1_at(nd, lo + 64u),
+                                                               ld1_at(nd, lo + 80u), r, inv, tmin, c, code);
+                        } else {
+                            hit = leaf_hit<kF, (kF & kFTri) == 0u, false, true>(S, lcode, r, q, tmin, c, code, inv);
+                        }
+                    } else {
+                        hit = leaf_hit<kF, (kF & kFTri) == 0u>(S, lcode, r, q, tmin, c, code, inv);
+                    }
+                    if (hit) {
                         // cube faces rank + 0..5 (the face leaf_hit's list walk kept)
                         const uint32_t rk = rank + (rtdev::leaf_type(lcode) == rtdev::kLeafCube
                                                         ? rtdev::leaf_index(code) - rtdev::leaf_index(lcode)
@@ -2835,11 +2912,13 @@ RT_DEV ReplayItem replay_take(const ReplayItem* list, uint32_t idx) {
     return ReplayItem{(uint32_t)v, (uint32_t)(v >> 32)};
 }
 constexpr uint32_t kReplayCap = 1u << 20;
-// A finished sample's radiance into the sample buffer (read once, by resolve_samples). RT_SBUF_NT
-// (A/B): non-temporal stores, so the 5.76 GB a C3 frame streams through do not evict the hot lines
-// (scene rows, register spills) from L2.
+// A finished sample's radiance into the sample buffer (read once, by resolve_samples). RT_SBUF_NT:
+// non-temporal stores, so the 5.76 GB a C3 frame streams through do not evict the hot lines (scene
+// rows, register spills) from L2. Measured (same box, 100-spp C3 / 50-spp C4 frames): C3 79.15 ->
+// 78.85 ms and 12.3 -> 8.9 GB of HBM traffic, C4 61.7 -> 61.6 ms and 63.8 -> 58.3 GB
+// (profiles/r06/experiments/sample_buffer_nt_and_waves_*). 0 builds plain stores (A/B).
 #ifndef RT_SBUF_NT
-#define RT_SBUF_NT 0
+#define RT_SBUF_NT 1
 #endif
 RT_DEV void sbuf_store(float* o, V L) {
     if constexpr (RT_SBUF_NT) {
@@ -4146,11 +4225,13 @@ int rt_render_launch_camera(rt_scene_handle s, const rt_camera* camera, const rt
     // for the BVH-only preset, whose 4-wave instance spills more than the extra wave buys
     // (same box, 3 vs 4 waves: C1 3.8 vs 4.1 ms; profiles/r05/experiments/waves_3v4_ab.log).
     // The triangle-BVH preset preferred 3 until round 5 (C4 at 50 spp 112.1 vs 121.4 ms in
-    // round 2); with the rect runs and scalar entry reads its 4-wave instance is 2.2% faster
-    // (1266 -> 1238 ms per frame). The Marble, sphere-run and flat presets stay at 4 (C3 +14%,
-    // C2 +12%, C5 +10% over 3; profiles/r02/w3/).
+    // round 2); with the rect runs and scalar entry reads its 4-wave instance became 2.2% faster
+    // (1266 -> 1238 ms per frame), and round 6 returned to 3: within 1% of the 4-wave speed (C4 at
+    // 50 spp 62.2 vs 61.7 ms) at an eighth of the HBM traffic (8.4 vs 63.8 GB per frame, the 4-wave
+    // instance's ~40 spilled VGPRs; profiles/r06/experiments/sample_buffer_nt_and_waves_*). The
+    // Marble, sphere-run and flat presets stay at 4 (C3 +12%, C2 +12%, C5 +10% over 3).
     const uint32_t preset_feats = s->features & ~kFDeep;
-    const bool prefer3 = preset_feats == kFBvh;
+    const bool prefer3 = preset_feats == kFBvh || preset_feats == (kFBvh | kFTri);
     // the cross-lane traversal's result keys behind the stack (bvh_run_shared), fast launch only
     const size_t share_lds = preset_shares(preset_of(s->features)) ? kShareKeyBytes : 0u;
     if (s->fast_waves == 0) {

@@ -961,6 +961,7 @@ class Lowerer {
                 if (c.node) return false;
             return true;
         };
+        bool cube_box_mismatch = false;  // (never: put's cube leaves read their leaf box as the cube)
         auto put = [&](uint32_t o, const std::vector<Slot>& sl, uint32_t flags) {
             float mnx[4], mny[4], mnz[4], mxx[4], mxy[4], mxz[4];
             uint32_t ch[4], rk[4];
@@ -991,6 +992,31 @@ class Lowerer {
             n[5] = {mxz[0], mxz[1], mxz[2], mxz[3]};
             n[6] = {bitsf(ch[0]), bitsf(ch[1]), bitsf(ch[2]), bitsf(ch[3])};
             n[7] = {bitsf(rk[0]), bitsf(rk[1]), bitsf(rk[2]), bitsf(rk[3])};
+            // A leaf node (1-2 object slots) carries its spheres in the lanes of the unused slots
+            // 2 / 3: slot k's sphere in component 2 + k of rows 0 (cx), 1 (cy), 2 (cz) and 6
+            // (radius), which the leaf test reads from the node's own line (kernel.hip bvh_run,
+            // RT_LEAF_EMBED) instead of from sph behind the child row. A cube needs nothing: its
+            // leaf box (prim_box, cube.rs:95-97) is exactly its six bounds.
+            bool leaf = sl.size() <= 2u;
+            for (const Slot& c : sl) leaf = leaf && !c.node;
+            for (uint32_t k = 0; leaf && k < sl.size(); ++k) {
+                const uint32_t code = sl[k].id, idx = rtdev::leaf_index(code);
+                auto lane = [&](int row) -> float& { return k ? n[row].w : n[row].z; };
+                if (rtdev::leaf_type(code) == rtdev::kLeafSphere) {
+                    const rtdev::f4 s = s_->sph[idx];
+                    lane(0) = s.x;
+                    lane(1) = s.y;
+                    lane(2) = s.z;
+                    lane(6) = s.w;
+                } else if (rtdev::leaf_type(code) == rtdev::kLeafCube) {
+                    const rtdev::f4 s0 = s_->rect[2 * (size_t)idx];
+                    const Box& b = sl[k].box;
+                    const float y1 = s_->rect[2 * (size_t)idx + 1].x, z1 = s_->rect[2 * (size_t)idx + 5].x;
+                    if (fbits(b.mn.x) != fbits(s0.y) || fbits(b.mn.y) != fbits(s0.w) || fbits(b.mn.z) != fbits(s0.x) ||
+                        fbits(b.mx.x) != fbits(s0.z) || fbits(b.mx.y) != fbits(y1) || fbits(b.mx.z) != fbits(z1))
+                        cube_box_mismatch = true;
+                }
+            }
         };
         // wrapper: slot 0 = the root (its box is tested on entry, bvh.rs:370);
         // its rank[3] carries the BVH's flags
@@ -1027,6 +1053,7 @@ class Lowerer {
             }
         }
         for (uint32_t w = 0; w < wide.size(); ++w) put(base + 1 + w, wide[w], 0u);
+        if (cube_box_mismatch) return fail(RT_ERR_UNSUPPORTED, "internal: a cube leaf's box is not its bounds");
         // The traversal stack a BVH4 walk needs at most: a visit of an interior node with k children
         // pushes the k - 1 it does not descend into first (2 words each) and descends into the
         // nearest, so need(w) = k - 1 + max need(child); a sibling popped later runs with fewer
