@@ -177,10 +177,6 @@ struct DevScene {
     // Material and texture records (32 B each) of a small scene, in that order; the flat-list
     // preset's fast kernel stages them in LDS when the launch sets mt_lds (their byte size).
     uint32_t num_mats, num_texs, mt_lds;
-    // Per BVH (base in its wrapper's rank[1]): the leaf code of each DFS ordinal, rank >> 3
-    // (lower.cpp bvh_emit); the cross-lane traversal (kernel.hip bvh_run_shared) recovers a
-    // hit's code from its rank.
-    const uint32_t* rank_code;
 };
 
 // Camera::new (camera.rs:44-81) evaluated on the host.

@@ -62,7 +62,7 @@ enum ProfRegion : uint32_t {
     kPrRefill = 0, kPrSegment, kPrWorld, kPrRecord, kPrEmit, kPrScatter, kPrMarble, kPrStore,
     kPrChecker, kPrImage, kPrUnitSphere, kPrDielectric, kPrLambert, kPrMetal, kPrIso, kPrLog,
     kPrEntry0 = 16, kPrEntryLast = 43, kPrBvhTrip = 44, kPrLeafTest = 45, kPrBvhSetup = 46, kPrBvhPush = 47,
-    kPrBvhPop = 48, kPrBvhCall = 49, kPrBvhSteal = 50, kPrCount = 52
+    kPrBvhPop = 48, kPrBvhCall = 49, kPrCount = 52
 };
 // traversal mode bits (bvh_hit): kModeExact = RT_FLAG_EXACT_BVH; the rest come
 // from DevParams::tune (rt_set_option(RT_OPT_TUNE), diagnostics / A-B runs).
@@ -709,28 +709,14 @@ constexpr uint32_t kFBvh = 1u, kFTri = 2u, kFRuns = 4u, kFDeep = 8u, kFLeafRM = 
 constexpr uint32_t kFSusp = 64u;
 
 [[maybe_unused]] constexpr uint32_t kStackLdsMax = 19u;  // LDS stack entries per lane at most (9.5 KB per wave: 16 waves/CU)
-// The cross-lane traversal of the sphere-BVH presets (bvh_run_shared; RT_SHARE=0 builds the
-// per-lane loop for A/B) keeps 64 result keys per wave behind the stack: 9728 + 512 B = 10 KB per
-// wave still fits 16 waves/CU (160 KB).
-#ifndef RT_SHARE
-#define RT_SHARE 0  // measured slower (C3 100 spp 83.3 -> 90.7 ms, C1 -7%: the denser issue lowered the clock)
-#endif
-// RT_SHARE_TRI (A/B): the triangle preset without the suspending walk, traversing across lanes
-#ifndef RT_SHARE_TRI
-#define RT_SHARE_TRI 0
-#endif
-constexpr uint32_t kShareKeyBytes = 64u * 8u;
-// The fast-kernel preset of a scene's features (fast_instance below) and whether it shares.
+// The fast-kernel preset of a scene's features (fast_instance below).
 constexpr uint32_t preset_of(uint32_t features) {
     return features == 0u                                        ? 0u
            : (features & ~kFRuns) == 0u                          ? kFRuns
            : (features & ~kFBvh) == 0u                           ? kFBvh
            : (features & ~(kFBvh | kFMarble)) == 0u              ? (kFBvh | kFMarble)
-           : (features & ~(kFBvh | kFTri | kFDeep)) == 0u        ? (kFBvh | kFTri | kFDeep | (RT_SHARE_TRI ? 0u : kFSusp))
+           : (features & ~(kFBvh | kFTri | kFDeep)) == 0u        ? (kFBvh | kFTri | kFDeep | kFSusp)
                                                                  : kFAll;
-}
-constexpr bool preset_shares(uint32_t preset) {
-    return RT_SHARE && (preset & kFBvh) != 0u && ((preset & kFTri) == 0u || (RT_SHARE_TRI && (preset & kFSusp) == 0u));
 }
 // One leaf (primitive or cube). tmax = closest so far; a hit with t == closest is
 // accepted, so later candidates win ties exactly like hittable.rs:110-116.
@@ -1303,21 +1289,13 @@ RT_DEV uint32_t ray_route(const Ray& r, V inv, float tmax_entry, const f4* wrapp
     return kRayHandOver;
 }
 
-template <uint32_t kF>
-RT_DEV bool bvh_run_shared(const DevScene& S, float delta, const f4* wrapper, uint32_t root, const Ray& r_own,
-                           V inv_own, float tmin_own, float& closest_io, uint32_t& hit_code, uint32_t* stk,
-                           uint32_t mode);
-template <uint32_t kF>
-constexpr bool kShare = preset_shares(kF);
 // RT_PEEL_WRAPPER: bvh_hit tests the wrapper's slot (the root box) before the traversal loop (0:
 // the loop's first trip does, A/B).
 #ifndef RT_PEEL_WRAPPER
 #define RT_PEEL_WRAPPER 1
 #endif
 constexpr bool kPeelWrapper = RT_PEEL_WRAPPER;
-// kTop: a top-level entry of the list walk (t_min = 0.001), where the sphere-BVH presets traverse
-// across lanes (bvh_run_shared); medium boundaries (t_min = -inf or t1 + 1e-4) keep bvh_run.
-template <int kKind, uint32_t kF = kFAll, bool kTop = false>
+template <int kKind, uint32_t kF = kFAll>
 RT_DEV bool bvh_hit(const DevScene& S, float delta, uint32_t root, const Ray& r, float tmin, float& closest,
                     uint32_t& hit_code, uint32_t* stk, uint32_t mode, bool& replay) {
     PROF_T0(pcall);
@@ -1354,9 +1332,7 @@ RT_DEV bool bvh_hit(const DevScene& S, float delta, uint32_t root, const Ray& r,
     }
     PROF_ADD(kPrBvhSetup, psetup);
     Trav tv{root, 0u, 0u, closest, false, kNoNode};
-    if constexpr (kKind == 0 && kTop && kShare<kF>) {
-        tv.any = bvh_run_shared<kF>(S, delta, wrapper, root, r, inv, tmin, closest, hit_code, stk, mode);
-    } else if constexpr (kPeelWrapper) {
+    if constexpr (kPeelWrapper) {
         // The wrapper's one slot (the root's box, bvh.rs:370) tested outside the loop, from scalar
         // loads at the wave-uniform wrapper address: the loop's first trip, which loads the same
         // rows for every lane with vector loads, sorts four keys of which three are empty and
@@ -1720,279 +1696,6 @@ RT_DEV bool bvh_run(const DevScene& S, float delta, const f4* wrapper, const Ray
     return finished;
 }
 
-// ---------------------------------------------------------------------------
-// Cross-lane BVH traversal (the sphere-BVH presets' top-level BVH calls, kShare<kF>).
-//
-// In a wave's call of a BVH, most lanes are done after the root test (C3: 78% of the lane
-// traversals visit one node) while the wave keeps looping for the few lanes with long
-// traversals: the child-test trips ran at 14.9 of 64 lanes (profiles/r05/regions_c3_64spp_*).
-// Here a lane whose traversal is done helps: each trip, the lanes with no work take the
-// pending stack entries (subtrees) of one traversing lane (the first one with any), together
-// with a copy of its ray, and traverse those subtrees on their own stacks. A traversal's
-// candidates are merged by (t, DFS rank) — smallest t, ties to the later leaf in the
-// reference's DFS order (bvh.rs:406-414) — which is a total order, so the winner does not
-// depend on which lane tested which leaf or in which order: every lane working on a ray
-// publishes each candidate it accepts into that ray's 64-bit key in LDS (ds_min_u64 of
-// t bits << 32 | ~rank; the calls here have t_min = 0.001 > 0, so positive float bits order
-// as u32), and reads the key back each trip to prune with the best candidate any lane found.
-// Every leaf node is still tested whole by one lane, exactly as in bvh_run (the left leaf
-// with the entry t_max, the right with the left hit's t, capped at nextup(closest) for a
-// closest >= the final one: the same winner, see bvh_run); pruning with any candidate's t is
-// conservative (exact-pruning argument). The hit's code comes from its rank through the BVH's
-// rank -> code table (lower.cpp bvh_emit, S.rank_code). LDS: 64 keys (512 B) behind the stack.
-constexpr unsigned long long kKeyNone = ~0ull;
-#ifndef RT_SHARE_REFRESH
-#define RT_SHARE_REFRESH 1  // (A/B) read the ray's best key back every trip, to prune with it
-#endif
-#ifndef RT_SHARE_MAXWORK
-#define RT_SHARE_MAXWORK 64  // (A/B) hand over only while at most this many lanes traverse
-#endif
-#ifndef RT_SHARE_MINSP
-#define RT_SHARE_MINSP 1  // (A/B) a donor has at least this many pending entries
-#endif
-RT_DEV unsigned long long share_key(float t, uint32_t rank) {
-    return ((unsigned long long)__float_as_uint(t) << 32) | (unsigned long long)(~rank);
-}
-template <uint32_t kF>
-RT_DEV bool bvh_run_shared(const DevScene& S, float delta, const f4* wrapper, uint32_t root, const Ray& r_own,
-                           V inv_own, float tmin_own, float& closest_io, uint32_t& hit_code, uint32_t* stk,
-                           uint32_t mode) {
-    const uint32_t lane = threadIdx.x;
-    uint32_t* const lds = stk - lane;  // the wave's LDS: stack[level][{node, t}][lane], then the keys
-    unsigned long long* const keys = reinterpret_cast<unsigned long long*>(lds + S.stack_depth * 128u);
-    keys[lane] = kKeyNone;
-    const uint32_t wflags = __float_as_uint(ld4c(wrapper + 7).w);
-    const bool prune = (wflags & rtdev::kBvhPrunable) != 0u || (kPruneAllExpBuild && (mode & kModePruneAllExp));
-    const bool leaf_boxes = prune && !(mode & kModeNoLeafBoxes);
-    // the traversal this lane works on: its own ray first, later a donor's
-    Ray r = r_own;
-    V inv = inv_own;
-    float tmin = tmin_own, tmax_entry = closest_io;
-    float closest = closest_io;  // this lane's bound: the best candidate known for the ray (or its t_max)
-    uint32_t best_rank = 0u, owner = lane, cur = root, sp = 0u;
-    bool working = true;
-    for (;;) {
-        // Hand-over: the idle lanes take the pending subtrees of the first lane that has any, top
-        // (nearest) first; the donor keeps the rest and its current node.
-        PROF_T0(psteal);
-        const unsigned long long idle = __ballot(!working);
-        if (idle != 0ull && (uint32_t)__popcll(idle) >= 64u - RT_SHARE_MAXWORK) {
-            const unsigned long long donors = __ballot(working && sp >= RT_SHARE_MINSP);
-            if (donors != 0ull) {
-                const uint32_t d = (uint32_t)__builtin_ctzll(donors);
-                const uint32_t dsp = __builtin_amdgcn_readlane(sp, d);
-                const uint32_t nidle = (uint32_t)__popcll(idle);
-                const uint32_t take = nidle < dsp ? nidle : dsp;
-                const uint32_t j = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
-                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
-                const float dox = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(r.o.x), d));
-                const float doy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(r.o.y), d));
-                const float doz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(r.o.z), d));
-                const float ddx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(r.d.x), d));
-                const float ddy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(r.d.y), d));
-                const float ddz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(r.d.z), d));
-                const float dtime = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(r.time), d));
-                const float dix = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(inv.x), d));
-                const float diy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(inv.y), d));
-                const float diz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(inv.z), d));
-                const float dtmin = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(tmin), d));
-                const float dtmax = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(tmax_entry), d));
-                const float dcl = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(closest), d));
-                const uint32_t drank = __builtin_amdgcn_readlane(best_rank, d);
-                const uint32_t down = __builtin_amdgcn_readlane(owner, d);
-                if (!working && j < take) {
-                    const uint32_t lvl = dsp - 1u - j;
-                    uint32_t node;
-                    float key;
-                    if (!(kF & kFDeep) || lvl < S.stack_depth) {
-                        node = lds[lvl * 128u + d];
-                        key = __uint_as_float(lds[lvl * 128u + 64u + d]);
-                    } else {  // the donor's entry in its wave's HBM slab (kFDeep: bvh_run's push)
-                        const uint32_t* g = S.stack_spill +
-                                            (((size_t)blockIdx.x * S.spill_depth + (lvl - S.stack_depth)) * 64u + d) * 2u;
-                        node = g[0];
-                        key = __uint_as_float(g[1]);
-                    }
-                    r.o = mk(dox, doy, doz);
-                    r.d = mk(ddx, ddy, ddz);
-                    r.time = dtime;
-                    inv = mk(dix, diy, diz);
-                    tmin = dtmin;
-                    tmax_entry = dtmax;
-                    closest = dcl;
-                    best_rank = drank;
-                    owner = down;
-                    sp = 0u;
-                    cur = node;
-                    working = !(prune && key > prune_bound(closest));  // the donor's pop would drop it
-                }
-                if (lane == d) sp = dsp - take;
-            }
-        }
-        PROF_ADD(kPrBvhSteal, psteal);
-        if (__ballot(working) == 0ull) break;
-        if (working) {
-            // the best candidate any lane found for this ray so far
-            if (RT_SHARE_REFRESH) {
-                const unsigned long long kb = keys[owner];
-                if (kb < share_key(closest, best_rank)) {
-                    closest = __uint_as_float((uint32_t)(kb >> 32));
-                    best_rank = ~(uint32_t)kb;
-                }
-            }
-            const float dmi = delta * fmaxf(fmaxf(__builtin_fabsf(inv.x), __builtin_fabsf(inv.y)), __builtin_fabsf(inv.z));
-            const bool cur_leaf = (cur & rtdev::kLeafNodeFlag) != 0u;
-            uint32_t onx, ony, onz;
-            {
-                uint32_t msx, msy, msz;  // 0 or ~0: 1/d < 0 on the axis (rederived per trip: bvh_run)
-                asm volatile("v_ashrrev_i32 %0, 31, %1" : "=v"(msx) : "v"(inv.x));
-                asm volatile("v_ashrrev_i32 %0, 31, %1" : "=v"(msy) : "v"(inv.y));
-                asm volatile("v_ashrrev_i32 %0, 31, %1" : "=v"(msz) : "v"(inv.z));
-                onx = msx & 48u;
-                ony = (msy & 48u) + 16u;
-                onz = (msz & 48u) + 32u;
-            }
-#ifdef RT_LEAF_AUDIT
-            if ((cur & ~rtdev::kLeafNodeFlag) >= S.num_nodes || sp > S.stack_depth) {
-                atomicAdd(&g_bounds_audit_count, 1u);
-                working = false;
-                continue;
-            }
-#endif
-            PROF_T0(pt);
-            if (cur_leaf) {  // bvh_run's leaf node: its BVH2 node's result formed as bvh.rs:377-414 does
-                const uint32_t nbo = (cur & ~rtdev::kLeafNodeFlag) * (rtdev::kBvhNodeF4 * 16u);
-                const f4* nd = S.nodes;
-                const float2 nx2 = ld2_at(nd, nbo + onx), ny2 = ld2_at(nd, nbo + ony), nz2 = ld2_at(nd, nbo + onz),
-                             fx2 = ld2_at(nd, nbo + (onx ^ 48u)), fy2 = ld2_at(nd, nbo + (ony ^ 80u)),
-                             fz2 = ld2_at(nd, nbo + (onz ^ 112u)), chs = ld2_at(nd, nbo + 96u), rks = ld2_at(nd, nbo + 112u);
-                float tmr = tmax_entry, nt = 0.0f;
-                bool nh = false;
-                uint32_t nrank = 0u;
-                const uint32_t nleaf = __float_as_uint(chs.y) == rtdev::kChildEmpty ? 1u : 2u;
-                float llo[2] = {-kInf, -kInf}, lhi[2] = {kInf, kInf};
-                if (leaf_boxes) leaf_intervals2_nf(nx2, ny2, nz2, fx2, fy2, fz2, r, inv, delta, llo, lhi);
-                for (uint32_t k = 0; k < nleaf; ++k) {
-                    const uint32_t lcode = __float_as_uint(k ? chs.y : chs.x), rank = __float_as_uint(k ? rks.y : rks.x);
-#ifdef RT_LEAF_AUDIT
-                    const float2 bx0 = ld2(S.nodes + nbo / 16u, 0), by0 = ld2(S.nodes + nbo / 16u, 1),
-                                 bz0 = ld2(S.nodes + nbo / 16u, 2), bx1 = ld2(S.nodes + nbo / 16u, 3),
-                                 by1 = ld2(S.nodes + nbo / 16u, 4), bz1 = ld2(S.nodes + nbo / 16u, 5);
-                    const float x0 = k ? bx0.y : bx0.x, y0 = k ? by0.y : by0.x, z0 = k ? bz0.y : bz0.x;
-                    const float x1 = k ? bx1.y : bx1.x, y1 = k ? by1.y : by1.x, z1 = k ? bz1.y : bz1.x;
-#endif
-                    const float bound = tmr < closest ? tmr : closest;
-                    if (!leaf_boxes || leaf_interval_may_hit(k ? llo[1] : llo[0], k ? lhi[1] : lhi[0], tmin, bound)) {
-                        PROF_T0(pl);
-                        const float cap = closest < kInf ? __uint_as_float(__float_as_uint(closest) + 1u) : kInf;
-                        float c = tmr < cap ? tmr : cap;
-                        uint32_t code = 0u;
-                        const RayD q = to_d(r);
-                        if (leaf_hit<kF, (kF & kFTri) == 0u>(S, lcode, r, q, tmin, c, code, inv)) {
-                            const uint32_t rk = rank + (rtdev::leaf_type(lcode) == rtdev::kLeafCube
-                                                            ? rtdev::leaf_index(code) - rtdev::leaf_index(lcode)
-                                                            : 0u);
-                            if (!nh || !(nt < c)) {
-                                nh = true;
-                                nt = c;
-                                nrank = rk;
-                            }
-                            tmr = c;
-                        }
-                        PROF_ADD(kPrLeafTest, pl);
-                    } else {
-                        LEAF_AUDIT(lcode, rank, x0, y0, z0, x1, y1, z1);
-                    }
-                }
-                if (nh && (nt < closest || (nt == closest && nrank > best_rank))) {
-                    closest = nt;
-                    best_rank = nrank;
-                    atomicMin(&keys[owner], share_key(nt, nrank));  // ds_min_u64: publish for the ray
-                }
-            }
-            float t0 = kInf, t1 = kInf, t2 = kInf, t3 = kInf;
-            uint32_t c0 = rtdev::kChildEmpty, c1 = rtdev::kChildEmpty, c2 = rtdev::kChildEmpty, c3 = rtdev::kChildEmpty;
-            if (!cur_leaf) {  // interior slots: reference box test, prune bound, nearest first (bvh_run)
-                const uint32_t nbo = cur * (rtdev::kBvhNodeF4 * 16u);
-                const f4* nd = S.nodes;
-                const f4 nx = ld4_at(nd, nbo + onx), ny = ld4_at(nd, nbo + ony), nz = ld4_at(nd, nbo + onz),
-                         fx = ld4_at(nd, nbo + (onx ^ 48u)), fy = ld4_at(nd, nbo + (ony ^ 80u)),
-                         fz = ld4_at(nd, nbo + (onz ^ 112u)), chf = ld4_at(nd, nbo + 96u);
-                c0 = __float_as_uint(chf.x);
-                c1 = __float_as_uint(chf.y);
-                c2 = __float_as_uint(chf.z);
-                c3 = __float_as_uint(chf.w);
-                float key[4];
-                child_keys4_nf(nx, ny, nz, fx, fy, fz, r, inv, tmin, tmax_entry, prune ? prune_bound(closest) : kInf,
-                               prune ? dmi : 0.0f, key);
-                t0 = key[0];
-                t1 = key[1];
-                t2 = key[2];
-                t3 = key[3];
-            }
-            PROF_ADD(kPrBvhTrip, pt);
-            PROF_T0(pp);
-            sort2(t0, c0, t1, c1);
-            sort2(t2, c2, t3, c3);
-            sort2(t0, c0, t2, c2);
-            sort2(t1, c1, t3, c3);
-            sort2(t1, c1, t2, c2);
-            auto push = [&](uint32_t node, float t) {  // (kFDeep: past stack_depth in the HBM slab, as bvh_run)
-                if (!(kF & kFDeep) || sp < S.stack_depth) {
-                    stk[sp * 128u] = node;
-                    stk[sp * 128u + 64u] = __float_as_uint(t);
-                } else {
-                    uint32_t* g = S.stack_spill +
-                                  (((size_t)blockIdx.x * S.spill_depth + (sp - S.stack_depth)) * 64u + lane) * 2u;
-                    g[0] = node;
-                    g[1] = __float_as_uint(t);
-                }
-                sp += 1u;
-            };
-            bool popnext = true;
-            if (t0 != kInf) {  // visit the nearest next, push the others far to near
-                if (t3 != kInf) push(c3, t3);
-                if (t2 != kInf) push(c2, t2);
-                if (t1 != kInf) push(c1, t1);
-                cur = c0;
-                popnext = false;
-            }
-            PROF_ADD(kPrBvhPush, pp);
-            PROF_T0(ppop);
-            if (popnext) {
-                bool found = false;
-                while (sp > 0u) {
-                    sp -= 1u;
-                    uint32_t cand;
-                    float tenter;
-                    if (!(kF & kFDeep) || sp < S.stack_depth) {
-                        cand = stk[sp * 128u];
-                        tenter = __uint_as_float(stk[sp * 128u + 64u]);
-                    } else {
-                        const uint32_t* g = S.stack_spill +
-                                            (((size_t)blockIdx.x * S.spill_depth + (sp - S.stack_depth)) * 64u + lane) * 2u;
-                        cand = g[0];
-                        tenter = __uint_as_float(g[1]);
-                    }
-                    if (!prune || !(tenter > prune_bound(closest))) {
-                        cur = cand;
-                        found = true;
-                        break;
-                    }
-                }
-                working = found;
-            }
-            PROF_ADD(kPrBvhPop, ppop);
-        }
-    }
-    const unsigned long long kb = keys[lane];
-    if (kb == kKeyNone) return false;
-    closest_io = __uint_as_float((uint32_t)(kb >> 32));
-    const uint32_t rank = ~(uint32_t)kb;
-    hit_code = S.rank_code[__float_as_uint(ld4c(wrapper + 7).y) + (rank >> 3)] + (rank & 7u);
-    return true;
-}
-
 // Translate (instance.rs:39) / RotateY (instance.rs:104-110, 121-124) applied to a ray.
 RT_DEV Ray apply_op(f4 op, Ray r) {
     if (op.w == 0.0f) {
@@ -2052,7 +1755,7 @@ constexpr uint32_t kRunPretestMin = 8u;  // sphere runs at least this long take 
 // A GEOM or BVH entry (the caller guarantees E is wave-uniform). Only instances
 // with kFRuns carry the f32 pretest of long sphere runs, only those with kFBvh the
 // BVH traversal (the host launches an instance whose features cover the scene's).
-template <int kKind, uint32_t kF, bool kTop = false>
+template <int kKind, uint32_t kF>
 RT_DEV bool entry_geom_hit(const DevScene& S, float delta, const DevEntry* E, Ray r, float tmin, float& closest,
                            uint32_t& hit_code, uint32_t* stk, uint32_t mode, bool& replay) {
     uint32_t ntf = uni<kF>(cst(E)->ntf);
@@ -2128,7 +1831,7 @@ RT_DEV bool entry_geom_hit(const DevScene& S, float delta, const DevEntry* E, Ra
             ABLATE(kAbBvh2, float c2 = closest; uint32_t h2 = 0u; bool rp = false;
                    if (bvh_hit<kKind, kF>(S, delta, cst(E)->payload, r, tmin, c2, h2, stk, mode, rp) && h2 == 0x7fffffffu)
                        closest = -1.0f;);
-            return bvh_hit<kKind, kF, kTop>(S, delta, uni<kF>(cst(E)->payload), r, tmin, closest, hit_code, stk, mode,
+            return bvh_hit<kKind, kF>(S, delta, uni<kF>(cst(E)->payload), r, tmin, closest, hit_code, stk, mode,
                                             replay);
         }
     }
@@ -2782,7 +2485,7 @@ RT_DEV bool world_hit(const DevScene& S, float delta, const Ray& r, Rng& g, cons
             }
         } else {
             uint32_t code;
-            if (entry_geom_hit<kKind, kF, true>(S, delta, E, r, 0.001f, closest, code, stk, mode, replay)) {
+            if (entry_geom_hit<kKind, kF>(S, delta, E, r, 0.001f, closest, code, stk, mode, replay)) {
                 hit_entry = e;
                 hit_code = code;
                 any = true;
@@ -3247,10 +2950,8 @@ __global__ __launch_bounds__(64, kWaves) void trace_samples(DevScene Sg, DevCame
     // Perlin permutation tables (Marble) behind the stack when they fit: the
     // three dependent byte lookups per lattice corner then hit LDS, not L2.
     DevScene S = Sg;
-    // (behind the cross-lane traversal's result keys in the presets that share, bvh_run_shared)
-    constexpr uint32_t kKeyWords = kKind == 0 && kShare<kF> ? kShareKeyBytes / 4u : 0u;
     if (S.perm_bytes != 0u && S.perm_bytes <= kPermLdsMax && !(P.tune & kModeNoPermLds)) {
-        uint32_t* tab = lds_stack + S.stack_depth * 128u + kKeyWords;
+        uint32_t* tab = lds_stack + S.stack_depth * 128u;
         const uint32_t* src = reinterpret_cast<const uint32_t*>(Sg.perm);
         for (uint32_t i = lane; i < S.perm_bytes / 4u; i += 64u) tab[i] = src[i];
         __syncthreads();
@@ -3708,8 +3409,8 @@ TraceKernel fast_instance(uint32_t features) {
         case kFRuns: return preset_instance<kWaves, kFRuns>();
         case kFBvh: return preset_instance<kWaves, kFBvh>();
         case kFBvh | kFMarble: return preset_instance<kWaves, kFBvh | kFMarble>();
-        case kFBvh | kFTri | kFDeep | (RT_SHARE_TRI ? 0u : kFSusp):
-            return preset_instance<kWaves, kFBvh | kFTri | kFDeep | (RT_SHARE_TRI ? 0u : kFSusp)>();
+        case kFBvh | kFTri | kFDeep | kFSusp:
+            return preset_instance<kWaves, kFBvh | kFTri | kFDeep | kFSusp>();
         default: return preset_instance<kWaves, kFAll>();
     }
 }
@@ -3798,7 +3499,6 @@ int rt_scene_upload(const rt_scene_desc* desc, int device, rt_scene_handle* out)
         {hs.nodes2.data(), hs.nodes2.size() * sizeof(f4), 0},
         {hs.hrpp_keys.data(), hs.hrpp_keys.size() * sizeof(uint64_t), 0},
         {hs.hrpp_vals.data(), hs.hrpp_vals.size() * sizeof(uint32_t), 0},
-        {hs.rank_code.data(), hs.rank_code.size() * sizeof(uint32_t), 0},
     };
     uint64_t total = 0;
     for (auto& p : parts) {
@@ -3859,7 +3559,6 @@ int rt_scene_upload(const rt_scene_desc* desc, int device, rt_scene_handle* out)
     d.hrpp_keys = (const unsigned long long*)(base + parts[12].off);
     d.hrpp_vals = (const uint32_t*)(base + parts[13].off);
     d.hrpp_nkeys = (uint32_t)hs.hrpp_keys.size();
-    d.rank_code = (const uint32_t*)(base + parts[14].off);
     d.hrpp_npred = hs.num_predictors;
     s->coord_bound = hs.coord_bound;
     d.rect_rcp_ok = 1u;  // div_rn_safe's scene half: rect / cube-side coordinates +0 or in [2^-20, 2^20]
@@ -4232,10 +3931,8 @@ int rt_render_launch_camera(rt_scene_handle s, const rt_camera* camera, const rt
     // Marble, sphere-run and flat presets stay at 4 (C3 +12%, C2 +12%, C5 +10% over 3).
     const uint32_t preset_feats = s->features & ~kFDeep;
     const bool prefer3 = preset_feats == kFBvh || preset_feats == (kFBvh | kFTri);
-    // the cross-lane traversal's result keys behind the stack (bvh_run_shared), fast launch only
-    const size_t share_lds = preset_shares(preset_of(s->features)) ? kShareKeyBytes : 0u;
     if (s->fast_waves == 0) {
-        const size_t stack_lds = (size_t)s->dev.stack_depth * 128u * sizeof(uint32_t) + share_lds;
+        const size_t stack_lds = (size_t)s->dev.stack_depth * 128u * sizeof(uint32_t);
         const size_t perm3 = s->dev.perm_bytes != 0u && s->dev.perm_bytes <= kPermLdsMax ? s->dev.perm_bytes : 0u;
         int per3 = 0, per4 = 0;
         const TraceKernel k3 = fast_instance(3, s->features), k4 = fast_instance(4, s->features);
@@ -4247,7 +3944,7 @@ int rt_render_launch_camera(rt_scene_handle s, const rt_camera* camera, const rt
     // LDS per wave: the kernel's traversal stack, then the Perlin tables
     const size_t perm_lds =
         s->dev.perm_bytes != 0u && s->dev.perm_bytes <= kPermLdsMax && !(dp.tune & kModeNoPermLds) ? s->dev.perm_bytes : 0u;
-    size_t lds = (size_t)s->dev.stack_depth * 128u * sizeof(uint32_t) + share_lds + perm_lds;
+    size_t lds = (size_t)s->dev.stack_depth * 128u * sizeof(uint32_t) + perm_lds;
     // the flat-list preset stages a small scene's materials and textures behind the stack (the fast
     // kernel's launch only: the reference and replay launches below reserve no LDS for them)
     const size_t mt_bytes = (size_t)(s->dev.num_mats + s->dev.num_texs) * 32u;

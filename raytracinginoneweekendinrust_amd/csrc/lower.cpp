@@ -30,7 +30,7 @@ uint64_t HostScene::bytes() const {
     return entries.size() * sizeof(rtdev::DevEntry) + sph.size() * 16 + sph_mat.size() * 4 +
            msph.size() * 16 + rect.size() * 16 + tri.size() * 16 + nodes.size() * 16 + nodes2.size() * 16 +
            mats.size() * sizeof(rtdev::DevMaterial) + texs.size() * sizeof(rtdev::DevTexture) +
-           perm.size() + texels.size() + hrpp_keys.size() * 8 + hrpp_vals.size() * 4 + rank_code.size() * 4;
+           perm.size() + texels.size() + hrpp_keys.size() * 8 + hrpp_vals.size() * 4;
 }
 
 // ---------------------------------------------------------------------------
@@ -761,20 +761,12 @@ class Lowerer {
         // in DFS order wins, bvh.rs:406-414).
         std::vector<uint32_t> rank(tn.size() * 2, 0);
         uint32_t ordinal = 0;
-        // the leaf code of each ordinal (the fast kernel's cross-lane traversal publishes only
-        // (t, rank) and recovers the code from the rank; a Cube face is its first side + face)
-        const uint32_t rank_base = (uint32_t)s_->rank_code.size();
-        s_->rank_code.push_back(0u);  // ordinal 0: unused
         std::function<void(uint32_t)> ranks = [&](uint32_t i) {
             for (int k = 0; k < 2; ++k) {
                 if (tn[i].is_node[k]) {
                     ranks(tn[i].child[k]);
                 } else if (tn[i].child[k] != rtdev::kChildEmpty) {
                     rank[2 * i + k] = (++ordinal) * 8u;
-                    const uint32_t c = tn[i].child[k];
-                    s_->rank_code.push_back(rtdev::leaf_type(c) == rtdev::kLeafCube
-                                                ? rtdev::leaf_code(rtdev::kLeafRect, rtdev::leaf_index(c))
-                                                : c);
                 }
             }
         };
@@ -1023,7 +1015,6 @@ class Lowerer {
         put(base, {Slot{true, wroot | 0x40000000u, tn[troot].box, 0u}},
             (prunable ? rtdev::kBvhPrunable : 0u) | (tri_only && !prunable ? rtdev::kBvhTriOnly : 0u));
         s_->nodes[(size_t)base * rtdev::kBvhNodeF4 + 7].z = bitsf(base2);  // wrapper rank[2]: the BVH2 wrapper
-        s_->nodes[(size_t)base * rtdev::kBvhNodeF4 + 7].y = bitsf(rank_base);  // rank[1]: its rank -> code table
         if (predictor) {  // Bvh::with_predictor (bvh.rs:69-80): HRPP side data
             // The predictor table stores, per ray hash, "leaf nodes" (GO_UP_LEVEL = 0,
             // bvh.rs:22: the BvhNode whose child object was hit). Each gets a

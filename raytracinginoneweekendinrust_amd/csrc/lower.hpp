@@ -18,9 +18,6 @@ struct HostScene {
     std::vector<rtdev::f4> sph;
     std::vector<uint32_t> sph_mat;
     std::vector<rtdev::f4> msph, rect, tri, nodes, nodes2;
-    // Per BVH, the leaf code of each DFS ordinal (rank >> 3) from the base in its wrapper's
-    // rank[1] (a Cube's entry is its first side's rect code: a face hit is that + rank & 7).
-    std::vector<uint32_t> rank_code;
     std::vector<rtdev::DevMaterial> mats;
     std::vector<rtdev::DevTexture> texs;
     std::vector<uint8_t> perm, texels;

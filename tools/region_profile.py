@@ -24,7 +24,7 @@ NAMES = ["Refill", "Finish segment", "World", "Record", "Emit", "Scatter", "Marb
          "UnitSphere", "Dielectric", "Lambert", "Metal", "Isotropic", "MediumLog"]
 COUNT = 52
 EXTRA = {44: "BVH loop trip (child tests)", 45: "BVH leaf test", 46: "BVH call setup", 47: "BVH sort + push",
-         48: "BVH pop loop", 49: "BVH call total", 50: "BVH hand-over (shared)"}
+         48: "BVH pop loop", 49: "BVH call total"}
 ENTRY0 = 16
 # showcase's top-level entries after lowering (lower.cpp merges consecutive top-level spheres into runs)
 SHOWCASE = ["boxes BVH", "light rect", "moving sphere", "sphere run (glass, metal, medium boundary)",

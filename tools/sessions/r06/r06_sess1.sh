@@ -1,5 +1,5 @@
 #!/usr/bin/env bash
-# Round 6, first call: the new multi-process cases (8 ranks on one GPU: the bench over ipc and shm,
+# Round 6 (run after call 9, on the library of commit 959aa23): the new multi-process cases (8 ranks on one GPU: the bench over ipc and shm,
 # the position-coded gather at world 8), then the whole GPU suite (with the round-6 zero-direction
 # cases on the triangle BVH), then the C3 and C4 bench lines.
 set -u
@@ -20,7 +20,8 @@ run() {  # run <log> <seconds> <cmd...>
     fi
 }
 run multiproc.log 900 python3 -u -m pytest tests/test_gpu_multiprocess.py -v --timeout 500 --timeout-method thread
-run gpu_tests.log 900 python3 -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread
+run gpu_tests.log 900 python3 -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread \
+    --ignore tests/test_gpu_multiprocess.py
 run bench_C3.log 300 python3 -u bench.py --config C3
 run bench_C4.log 300 python3 -u bench.py --config C4
 echo "== done" | tee -a "$OUT/session.log"
