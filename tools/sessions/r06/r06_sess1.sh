@@ -1,5 +1,5 @@
 #!/usr/bin/env bash
-# Round 6 (run after call 9, on the library of commit 959aa23): the new multi-process cases (8 ranks on one GPU: the bench over ipc and shm,
+# Round 6 (run after call 9, on the library of commit a15b17a, md5 a50038f8...): the new multi-process cases (8 ranks on one GPU: the bench over ipc and shm,
 # the position-coded gather at world 8), then the whole GPU suite (with the round-6 zero-direction
 # cases on the triangle BVH), then the C3 and C4 bench lines.
 set -u
