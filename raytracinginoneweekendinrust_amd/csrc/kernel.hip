@@ -1266,16 +1266,19 @@ constexpr uint32_t kRayFast = 0u, kRayHandOver = 1u, kRayNoHit = 2u;
 // Where: the relaxed rule for triangle-only BVHs is compiled into the replay pass (kKind 3) only,
 // which re-traces the handed-over samples from their camera ray: their zero-direction rays then
 // take its fast traversal instead of the literal recursion over the unpruned mesh (C4's replay
-// tail). In the fast kernel the same code cost the triangle preset's register allocation 10% (C4
-// 50 spp 62.0 vs 68.8 ms, profiles/r06/experiments/ray_route_ab_c4.log) for a few hundred samples
-// per frame, so it hands those over as before.
+// tail). In the fast kernel the same code cost the triangle preset's 4-wave instance 10% (C4
+// 50 spp 62.0 vs 68.8 ms, profiles/r06/experiments/ray_route_zero_direction_ab.log), so it hands
+// those over as before; RT_TRI_ZERO_DIR_FAST 1 compiles the rule into the fast kernel too (A/B).
+#ifndef RT_TRI_ZERO_DIR_FAST
+#define RT_TRI_ZERO_DIR_FAST 0
+#endif
 template <int kKind, uint32_t kF>
 RT_DEV uint32_t ray_route(const Ray& r, V inv, float tmax_entry, const f4* wrapper, uint32_t mode) {
     const float ax = __builtin_fabsf(inv.x), ay = __builtin_fabsf(inv.y), az = __builtin_fabsf(inv.z);
     const bool ofin = __builtin_fabsf(r.o.x) < kInf && __builtin_fabsf(r.o.y) < kInf && __builtin_fabsf(r.o.z) < kInf;
     const bool tnum = tmax_entry == tmax_entry;
     if (ax > 0.0f && ax < kInf && ay > 0.0f && ay < kInf && az > 0.0f && az < kInf && ofin && tnum) return kRayFast;
-    if constexpr ((kF & kFTri) != 0u && kKind == 3) {
+    if constexpr ((kF & kFTri) != 0u && (kKind == 3 || (kKind == 0 && RT_TRI_ZERO_DIR_FAST))) {
         if ((__float_as_uint(ld4c(wrapper + 7).w) & rtdev::kBvhTriOnly) != 0u &&
             !(kPruneAllExpBuild && (mode & kModePruneAllExp))) {
             if (r.o.x != r.o.x || r.o.y != r.o.y || r.o.z != r.o.z || r.d.x != r.d.x || r.d.y != r.d.y ||
@@ -2538,7 +2541,12 @@ RT_DEV void world_walk(const DevScene& S, float delta, const Ray& ray, Rng& g, c
             const f4* wrapper = S.nodes + (size_t)root * rtdev::kBvhNodeF4;
             const V inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
             if (!w.resume) {  // bvh_hit's hand-over rule (NaN-prone rays go to the reference kernel)
-                if (ray_route<0, kF>(r, inv, w.closest, wrapper, mode) != kRayFast) {
+                const uint32_t route = ray_route<0, kF>(r, inv, w.closest, wrapper, mode);
+                if (route == kRayNoHit) {  // (RT_TRI_ZERO_DIR_FAST) a NaN ray: the mesh returns no hit
+                    w.pos = e + 1u;
+                    continue;
+                }
+                if (route != kRayFast) {
                     replay = true;
                     w.pos = S.num_top + 1u;  // abandoned: the sample is re-traced by the reference kernel
                     continue;
