@@ -726,7 +726,7 @@ RT_DEV f4 ldt(const f4* p) {
     if constexpr (kC) return ld4c(p);
     return ld4(p);
 }
-// RT_LEAF_EMBED: the BVH leaf test reads a leaf node's spheres (cx, cy, cz, r; lower.cpp put
+// RT_LEAF_EMBED: the BVH leaf test reads a leaf node's spheres (cx, cy, cz, r; lower.cpp
 // repeats them in the free slot lanes) and its cubes' bounds (a cube's leaf box is exactly its
 // bounds) from the node's own rows, so it no longer waits on a second, dependent load from sph /
 // rect, nor holds those scene pointers across the traversal loop. 0 builds the round-5 leaf
@@ -1263,14 +1263,16 @@ RT_DEV bool bvh_run(const DevScene& S, float delta, const f4* wrapper, const Ray
 // direction; a NaN closest_so_far, e.g. from a 0/0 rect hit earlier in the list whose plane axis
 // the BVH's own frame rotated away).
 constexpr uint32_t kRayFast = 0u, kRayHandOver = 1u, kRayNoHit = 2u;
-// Where: the relaxed rule for triangle-only BVHs is compiled into the replay pass (kKind 3) only,
-// which re-traces the handed-over samples from their camera ray: their zero-direction rays then
-// take its fast traversal instead of the literal recursion over the unpruned mesh (C4's replay
-// tail). In the fast kernel the same code cost the triangle preset's 4-wave instance 10% (C4
-// 50 spp 62.0 vs 68.8 ms, profiles/r06/experiments/ray_route_zero_direction_ab.log), so it hands
-// those over as before; RT_TRI_ZERO_DIR_FAST 1 compiles the rule into the fast kernel too (A/B).
+// Where: the relaxed rule for triangle-only BVHs is compiled into the replay pass (kKind 3), which
+// re-traces handed-over samples from their camera ray, and (RT_TRI_ZERO_DIR_FAST 1, the default)
+// into the fast kernel. In the fast kernel's 4-wave triangle instance the code cost 10% (C4 50 spp
+// 62.0 vs 68.8 ms, profiles/r06/experiments/ray_route_zero_direction_ab.log); in the spill-free
+// 3-wave instance the product runs since, it costs 0.7% of the fast kernel and removes C4's
+// handed-over samples, whose re-traced paths ended 0-25 ms after the fast kernel (full C4 frame
+// 1113 ms every run against 1111-1137 ms, profiles/r06/experiments/zero_direction_fast_kernel_ab.log).
+// 0 builds the replay-pass-only rule (A/B).
 #ifndef RT_TRI_ZERO_DIR_FAST
-#define RT_TRI_ZERO_DIR_FAST 0
+#define RT_TRI_ZERO_DIR_FAST 1
 #endif
 template <int kKind, uint32_t kF>
 RT_DEV uint32_t ray_route(const Ray& r, V inv, float tmax_entry, const f4* wrapper, uint32_t mode) {
@@ -2542,9 +2544,11 @@ RT_DEV void world_walk(const DevScene& S, float delta, const Ray& ray, Rng& g, c
             const V inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
             if (!w.resume) {  // bvh_hit's hand-over rule (NaN-prone rays go to the reference kernel)
                 const uint32_t route = ray_route<0, kF>(r, inv, w.closest, wrapper, mode);
-                if (route == kRayNoHit) {  // (RT_TRI_ZERO_DIR_FAST) a NaN ray: the mesh returns no hit
-                    w.pos = e + 1u;
-                    continue;
+                if constexpr (RT_TRI_ZERO_DIR_FAST && (kF & kFTri) != 0u) {
+                    if (route == kRayNoHit) {  // a NaN ray: the mesh returns no hit (bvh_hit's answer)
+                        w.pos = e + 1u;
+                        continue;
+                    }
                 }
                 if (route != kRayFast) {
                     replay = true;

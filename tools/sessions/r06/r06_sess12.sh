@@ -21,7 +21,7 @@ run() {  # run <log> <seconds> <cmd...>
     fi
 }
 L=raytracinginoneweekendinrust_amd/_lib
-run ab.log 600 bash tools/ab_session.sh r06_zdfast "C4:50 C4" $L/librtamd.so $L/librtamd_zdfast.so
+run ab.log 600 bash tools/ab_session.sh r06_zdfast "C4:50 C4" $L/librtamd_a15.so $L/librtamd.so $L/librtamd_zdfast.so
 run parity.log 900 env RT_LIBRARY=$L/librtamd_zdfast.so python3 -u -m pytest tests/test_gpu_parity.py -x -v --timeout 300 \
     --timeout-method thread -k "C4 or zero_direction or every_feature or streaming or replay"
 run kats.log 300 env RT_LIBRARY=$L/librtamd_zdfast.so python3 -u -m pytest tests/test_gpu_kats.py -x -v --timeout 120 \
