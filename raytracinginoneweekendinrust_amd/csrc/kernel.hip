@@ -2631,12 +2631,17 @@ constexpr uint32_t kReplayCap = 1u << 20;
 // non-temporal stores, so the 5.76 GB a C3 frame streams through do not evict the hot lines (scene
 // rows, register spills) from L2. Measured (same box, 100-spp C3 / 50-spp C4 frames): C3 79.15 ->
 // 78.85 ms and 12.3 -> 8.9 GB of HBM traffic, C4 61.7 -> 61.6 ms and 63.8 -> 58.3 GB
-// (profiles/r06/experiments/sample_buffer_nt_and_waves_*). 0 builds plain stores (A/B).
+// (profiles/r06/experiments/sample_buffer_nt_and_waves_*). The flat-list presets (C2, C5) keep plain
+// stores: there the non-temporal form doubled the sample buffer's HBM writes (C2 7.5 -> 11.8 GB,
+// C5 83 -> 118 GB per frame: 12-byte records written around L2) at equal speed
+// (mc_schedulers_and_nt_bvh_only_ab.log). RT_SBUF_NT 2: non-temporal in the BVH presets only (the
+// product); 1: every preset; 0: plain stores everywhere (A/B).
 #ifndef RT_SBUF_NT
-#define RT_SBUF_NT 1
+#define RT_SBUF_NT 2
 #endif
+template <uint32_t kF = kFAll>
 RT_DEV void sbuf_store(float* o, V L) {
-    if constexpr (RT_SBUF_NT) {
+    if constexpr (RT_SBUF_NT == 1 || (RT_SBUF_NT == 2 && (kF & kFBvh) != 0u)) {
         __builtin_nontemporal_store(L.x, o);
         __builtin_nontemporal_store(L.y, o + 1);
         __builtin_nontemporal_store(L.z, o + 2);
@@ -2861,7 +2866,7 @@ RT_DEV bool finish_segment(const DevScene& S, const DevParams& P, const ChunkPar
         }
     }
     if (done) {
-        sbuf_store(sbuf + ((size_t)s_local * Q.nslots + slot) * 3u, L);
+        sbuf_store<kF>(sbuf + ((size_t)s_local * Q.nslots + slot) * 3u, L);
     }
     PROF_ADD(kPrSegment, pg);
     return done;
@@ -2926,7 +2931,7 @@ RT_DEV bool shade_marble(const DevScene& S, const DevParams& P, const ChunkParam
         else if (scattered) T = T * mk(sv, sv, sv);
     }
     if (shade && done) {
-        sbuf_store(sbuf + ((size_t)s_local * Q.nslots + slot) * 3u, L);
+        sbuf_store<kF>(sbuf + ((size_t)s_local * Q.nslots + slot) * 3u, L);
     }
     return shade && done;
 }

@@ -1,8 +1,9 @@
 #!/usr/bin/env bash
-# Round 6, calls 10-11: the evidence set for the round's final library (commit a15b17a, md5 a50038f8...):
-# call 10 = the rocprofv3 kernel trace + PMC passes of every config and the PMC summaries
-# (profiles/r06/pmc_*_C*.json); call 11 = one bench line per config, the driver-style C3 line,
-# the GPU suite and smoke(). Both through tools/final_evidence.sh.
+# Round 6, the evidence set for a final library through tools/final_evidence.sh: `profiles` = the rocprofv3
+# kernel trace + PMC passes of every config and the PMC summaries (profiles/r06/pmc_*_C*.json); `bench` =
+# one bench line per config, the driver-style C3 line, the GPU suite (multi-process tests included) and
+# smoke(). Calls 10/11 ran it on a15b17a (md5 a50038f8...), calls 14/15 on the final library (the fast-kernel
+# zero-direction rule, non-temporal sample-buffer stores in the BVH presets only).
 set -u
 cd "$(dirname "$0")/../../.."
 ROUND=r06 bash tools/final_evidence.sh "${1:-profiles}"
