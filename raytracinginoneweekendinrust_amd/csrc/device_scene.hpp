@@ -42,9 +42,6 @@ constexpr uint32_t kBvhPrunable = 1u;  // wrapper-node flag: closest-hit box pru
 // use no delta-inflation, and the fast kernel traverses it also with a zero direction component
 // (kernel.hip ray_route).
 constexpr uint32_t kBvhTriOnly = 2u;
-// BVH4 wrapper flag: every leaf is a Sphere (kernel.hip bvh_run: the A/B build RT_POSTPONE_SPH postpones
-// leaf tests in such BVHs only).
-constexpr uint32_t kBvhSphOnly = 4u;
 // BVH2 wrapper flag (nodes2 wrapper row 3 .w): every leaf is a Tri. Möller-Trumbore
 // (triangle.rs:32-92) rejects any ray with a NaN origin or direction component (a NaN
 // reaches t, and !(t > EPSILON) rejects it), so such a BVH returns no hit for that ray

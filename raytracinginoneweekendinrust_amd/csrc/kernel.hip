@@ -1236,12 +1236,6 @@ constexpr uint32_t kSuspMinTrips = RT_SUSP_MIN_TRIPS;
 #ifndef RT_LEAF_Q
 #define RT_LEAF_Q 8
 #endif
-#ifndef RT_POSTPONE_SPH
-#define RT_POSTPONE_SPH 0
-#endif
-#ifndef RT_SPH_Q
-#define RT_SPH_Q 8
-#endif
 
 template <int kKind, uint32_t kF, bool kSusp>
 RT_DEV bool bvh_run(const DevScene& S, float delta, const f4* wrapper, const Ray& r, V inv, float tmin, float& closest,
@@ -1412,16 +1406,9 @@ RT_DEV bool bvh_run(const DevScene& S, float delta, const f4* wrapper, const Ray
     // leaf hit prunes the rest of the stack, no q beat testing at once (runtime-q build: C3 q = 8
     // -1.4%, C1 -3%), so they compile the immediate loop, instruction for instruction the old one
     // (profiles/r04/experiments/leaf_postpone_*.log).
-    // RT_POSTPONE_SPH 1 (A/B): the sphere-BVH presets compile the postponing loop too and postpone in
-    // BVHs whose every leaf is a sphere (kBvhSphOnly: C3's sphere cluster), at q = RT_SPH_Q sixteenths
-    // (RT_OPT_TUNE bits 24-27 override it); other BVHs run it with q = 0 (test each leaf at once).
-    constexpr bool kPostpone = kKind == 0 && ((kF & kFTri) != 0u || (RT_POSTPONE_SPH && (kF & kFBvh) != 0u));
+    constexpr bool kPostpone = (kF & kFTri) != 0u && kKind == 0;
     const uint32_t tq = (mode >> 24) & 15u;
-    uint32_t lq = !kPostpone ? 0u : (tq == 15u ? 0u : (tq ? tq : (uint32_t)RT_LEAF_Q));
-    if constexpr (kPostpone && (kF & kFTri) == 0u) {
-        if ((__float_as_uint(ld4c(wrapper + 7).w) & rtdev::kBvhSphOnly) == 0u) lq = 0u;
-        else if (!tq) lq = RT_SPH_Q;
-    }
+    const uint32_t lq = !kPostpone ? 0u : (tq == 15u ? 0u : (tq ? tq : (uint32_t)RT_LEAF_Q));
     bool finished = true;
     [[maybe_unused]] uint32_t trips = 0;
 #ifdef RT_PROFILE_REGIONS

@@ -929,13 +929,11 @@ class Lowerer {
         };
         const Box none2{{0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f}};
         put2(base2, tn[troot].box, none2, remap2[troot], rtdev::kChildEmpty);
-        bool tri_only = true, sph_only = true;
+        bool tri_only = true;
         for (const TNode& t : tn)
             for (int k = 0; k < 2; ++k)
-                if (!t.is_node[k] && t.child[k] != rtdev::kChildEmpty) {
-                    if (rtdev::leaf_type(t.child[k]) != rtdev::kLeafTri) tri_only = false;
-                    if (rtdev::leaf_type(t.child[k]) != rtdev::kLeafSphere) sph_only = false;
-                }
+                if (!t.is_node[k] && t.child[k] != rtdev::kChildEmpty && rtdev::leaf_type(t.child[k]) != rtdev::kLeafTri)
+                    tri_only = false;
         s_->nodes2[4 * (size_t)base2 + 3].w = bitsf(tri_only ? rtdev::kBvh2TriOnly : 0u);
         for (uint32_t i = 0; i < tn.size(); ++i) {
             Box cb[2];
@@ -1015,8 +1013,7 @@ class Lowerer {
         // wrapper: slot 0 = the root (its box is tested on entry, bvh.rs:370);
         // its rank[3] carries the BVH's flags
         put(base, {Slot{true, wroot | 0x40000000u, tn[troot].box, 0u}},
-            (prunable ? rtdev::kBvhPrunable : 0u) | (tri_only && !prunable ? rtdev::kBvhTriOnly : 0u) |
-                (sph_only ? rtdev::kBvhSphOnly : 0u));
+            (prunable ? rtdev::kBvhPrunable : 0u) | (tri_only && !prunable ? rtdev::kBvhTriOnly : 0u));
         s_->nodes[(size_t)base * rtdev::kBvhNodeF4 + 7].z = bitsf(base2);  // wrapper rank[2]: the BVH2 wrapper
         if (predictor) {  // Bvh::with_predictor (bvh.rs:69-80): HRPP side data
             // The predictor table stores, per ray hash, "leaf nodes" (GO_UP_LEVEL = 0,
