@@ -42,6 +42,9 @@ constexpr uint32_t kBvhPrunable = 1u;  // wrapper-node flag: closest-hit box pru
 // use no delta-inflation, and the fast kernel traverses it also with a zero direction component
 // (kernel.hip ray_route).
 constexpr uint32_t kBvhTriOnly = 2u;
+// Such a BVH also carries its leaf codes in DFS order behind its nodes (lower.cpp bvh_emit; first
+// node index in the wrapper's rank[1]); kDfsPairLeft marks the left object of a two-object leaf node.
+constexpr uint32_t kDfsPairLeft = 0x80000000u;
 // BVH2 wrapper flag (nodes2 wrapper row 3 .w): every leaf is a Tri. Möller-Trumbore
 // (triangle.rs:32-92) rejects any ray with a NaN origin or direction component (a NaN
 // reaches t, and !(t > EPSILON) rejects it), so such a BVH returns no hit for that ray

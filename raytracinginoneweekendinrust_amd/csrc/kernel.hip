@@ -1294,6 +1294,56 @@ RT_DEV uint32_t ray_route(const Ray& r, V inv, float tmax_entry, const f4* wrapp
     return kRayHandOver;
 }
 
+// A triangle-only BVH entered with a NaN closest_so_far, in the replay pass (bvh_hit, kKind 3), for a
+// ray with a finite origin and direction. With t_max = NaN every reference box test passes
+// (aabb.rs:28-41: `t1 < t_max` and `t_max <= t_min` are false), and BvhNode::hit (bvh.rs:363-417)
+// passes its own t_max to both Index children (only a leaf's right object gets the left object's t),
+// so the t_max stays NaN on every level: every leaf node is visited and the tree keeps, by
+// `if l.t < r.t {l} else {r}`, the least t with ties going to the later object in DFS order. A leaf
+// node's left object is tested against NaN (Moller-Trumbore, triangle.rs:32-92, then accepts any
+// t >= t_min, t > EPSILON) and its right one against the left's t when the left hit (else NaN). So
+// the answer is a scan of the BVH's leaf objects in DFS order (lower.cpp bvh_emit's table), no box
+// test at all: the same arithmetic per triangle, the same selection, as the literal recursion
+// (oracle.c bvh_node_hit), which visited every node of C4's 20k-triangle tree from one lane (~20 ms a
+// segment: the replay pass's tail after C4's fast kernel) where the scan's loads do not wait on each
+// other.
+template <uint32_t kF>
+RT_DEV bool bvh_hit_nan_tmax(const DevScene& S, const f4* wrapper, const Ray& r, float tmin, float& closest,
+                             uint32_t& hit_code) {
+    const f4* T = S.nodes + (size_t)__float_as_uint(ld4c(wrapper + 7).y) * rtdev::kBvhNodeF4;
+    const uint32_t n = __float_as_uint(ld1_at(T, 0u));
+    const float nan = __uint_as_float(0x7fc00000u);
+    bool any = false;
+    float best = 0.0f;
+    uint32_t best_code = 0u;
+    auto test = [&](uint32_t i, float tmax, float& t) {
+        const uint32_t idx = rtdev::leaf_index(__float_as_uint(ld1_at(T, 16u + 4u * i)));
+        return tri_t(ld4(S.tri + 3 * (size_t)idx), ld4(S.tri + 3 * (size_t)idx + 1), ld4(S.tri + 3 * (size_t)idx + 2), r,
+                     tmin, tmax, t);
+    };
+    for (uint32_t i = 0; i < n;) {
+        const uint32_t e = __float_as_uint(ld1_at(T, 16u + 4u * i));
+        const bool pair = (e & rtdev::kDfsPairLeft) != 0u && i + 1u < n;
+        float tl = 0.0f, tr = 0.0f;
+        const bool hl = test(i, nan, tl);
+        const bool hr = pair && test(i + 1u, hl ? tl : nan, tr);
+        // the leaf node's result: its right object when that hit (then tr <= tl), else its left one
+        if (hl || hr) {
+            const float t = hr ? tr : tl;
+            if (!any || !(best < t)) {  // the tree's `l.t < r.t ? l : r`, the earlier nodes on the left
+                any = true;
+                best = t;
+                best_code = __float_as_uint(ld1_at(T, 16u + 4u * (hr ? i + 1u : i))) & ~rtdev::kDfsPairLeft;
+            }
+        }
+        i += pair ? 2u : 1u;
+    }
+    if (!any) return false;
+    closest = best;
+    hit_code = best_code;
+    return true;
+}
+
 // RT_PEEL_WRAPPER: bvh_hit tests the wrapper's slot (the root box) before the traversal loop (0:
 // the loop's first trip does, A/B).
 #ifndef RT_PEEL_WRAPPER
@@ -1326,9 +1376,19 @@ RT_DEV bool bvh_hit(const DevScene& S, float delta, uint32_t root, const Ray& r,
         const uint32_t route = ray_route<kKind, kF>(r, inv, closest, wrapper, mode);
         if (route == kRayNoHit) return false;
         if constexpr (kKind == 3) {
-            if (route == kRayHandOver)
+            if (route == kRayHandOver) {
+                if constexpr ((kF & kFTri) != 0u) {
+                    const bool fin = __builtin_fabsf(r.o.x) < kInf && __builtin_fabsf(r.o.y) < kInf &&
+                                     __builtin_fabsf(r.o.z) < kInf && __builtin_fabsf(r.d.x) < kInf &&
+                                     __builtin_fabsf(r.d.y) < kInf && __builtin_fabsf(r.d.z) < kInf;
+                    if (closest != closest && fin &&
+                        (__float_as_uint(ld4c(wrapper + 7).w) & rtdev::kBvhTriOnly) != 0u &&
+                        !(kPruneAllExpBuild && (mode & kModePruneAllExp)))
+                        return bvh_hit_nan_tmax<kF>(S, wrapper, r, tmin, closest, hit_code);
+                }
                 return bvh_hit_reference(S, __float_as_uint(ld4c(wrapper + 7).z), r, to_d(r), inv, tmin, closest, hit_code,
                                          stk);
+            }
         }
         if (route == kRayHandOver) {
             replay = true;

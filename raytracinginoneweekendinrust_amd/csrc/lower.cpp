@@ -761,12 +761,17 @@ class Lowerer {
         // in DFS order wins, bvh.rs:406-414).
         std::vector<uint32_t> rank(tn.size() * 2, 0);
         uint32_t ordinal = 0;
+        // the leaf codes in DFS order, bit 31 on the left object of a two-object leaf node (the leaf
+        // scan of a triangle BVH entered with a NaN t_max, kernel.hip bvh_hit_nan_tmax)
+        std::vector<uint32_t> dfs;
         std::function<void(uint32_t)> ranks = [&](uint32_t i) {
             for (int k = 0; k < 2; ++k) {
                 if (tn[i].is_node[k]) {
                     ranks(tn[i].child[k]);
                 } else if (tn[i].child[k] != rtdev::kChildEmpty) {
                     rank[2 * i + k] = (++ordinal) * 8u;
+                    const bool pair_left = k == 0 && !tn[i].is_node[1] && tn[i].child[1] != rtdev::kChildEmpty;
+                    dfs.push_back(tn[i].child[k] | (pair_left ? rtdev::kDfsPairLeft : 0u));
                 }
             }
         };
@@ -1062,6 +1067,22 @@ class Lowerer {
         s_->max_stack = std::max(s_->max_stack, need.empty() ? 1u : std::max(1u, need[0]));
         s_->max_stack_ref = std::max(s_->max_stack_ref, 2u * (max_depth_ + 2u));
         s_->max_bvh_depth = std::max(s_->max_bvh_depth, max_depth_ + 1);
+        if (tri_only && !prunable) {
+            // A triangle-only BVH's leaf codes in DFS order behind its nodes (whole 8-row nodes: row 0 .x
+            // = the count, then four codes a row), its first node index in the wrapper's rank[1].
+            const uint32_t tab = (uint32_t)(s_->nodes.size() / rtdev::kBvhNodeF4);
+            const size_t rows = 1 + (dfs.size() + 3) / 4;
+            const uint32_t nn = (uint32_t)((rows + rtdev::kBvhNodeF4 - 1) / rtdev::kBvhNodeF4);
+            if (tab + nn >= (rtdev::kLeafNodeFlag >> 1)) return fail(RT_ERR_UNSUPPORTED, "too many BVH nodes");
+            s_->nodes.resize((size_t)(tab + nn) * rtdev::kBvhNodeF4, rtdev::f4{0.0f, 0.0f, 0.0f, 0.0f});
+            rtdev::f4* T = &s_->nodes[(size_t)tab * rtdev::kBvhNodeF4];
+            T[0].x = bitsf((uint32_t)dfs.size());
+            for (size_t i = 0; i < dfs.size(); ++i) {
+                rtdev::f4& row = T[1 + i / 4];
+                (i % 4 == 0 ? row.x : i % 4 == 1 ? row.y : i % 4 == 2 ? row.z : row.w) = bitsf(dfs[i]);
+            }
+            s_->nodes[(size_t)base * rtdev::kBvhNodeF4 + 7].y = bitsf(tab);  // wrapper rank[1]
+        }
         *root_out = base;
         return RT_OK;
     }

@@ -256,6 +256,52 @@ def test_zero_direction_component_on_the_triangle_bvh(case, suspend, rt, orc, ca
     assert replayed == (0 if case == "zero_dx" else 48 * 36 * 3), (replayed, err[-2000:])
 
 
+@pytest.mark.parametrize("suspend", [True, False])
+def test_nan_closest_rays_that_hit_the_triangle_bvh(suspend, rt, orc, capfd):
+    # A triangle-only BVH entered with a NaN closest_so_far, where the rays do hit triangles (the
+    # "nan_closest" case above only has rays that miss the mesh): an xy_rect at z = 200 first in the
+    # list gives every camera ray of a fan in the plane z = 200 the hit (k - o) / d = 0 / 0 = NaN
+    # (rectangle.rs:36-65 accepts it), then the mesh BVH, whose triangles straddle that plane. The
+    # fast kernel hands every sample over; the replay pass takes kernel.hip bvh_hit_nan_tmax (the
+    # leaf scan in DFS order up to the first hit, then the fast traversal) instead of the literal
+    # recursion. Bits and segment counts must be the oracle's; `suspend` False adds a sphere run
+    # (the all-features instance).
+    b = rt.SceneBuilder()
+    white = b.lambertian_from_color((0.73, 0.73, 0.73))
+    red = b.lambertian_from_color((0.65, 0.05, 0.05))
+    light = b.diffuse_light_from_color((15.0, 15.0, 15.0))
+    w = rt.HittableList()
+    w.add(b.xy_rect(0, 555, 0, 555, 200, white))
+    w.add(b.xz_rect(213, 343, 227, 332, 554, light))
+    mesh = rt.HittableList()
+    rng = np.random.default_rng(5)
+    for _ in range(400):
+        c = rng.uniform((120, 40, 170), (440, 520, 230))
+        e = rng.uniform(-45, 45, size=(2, 3))
+        mesh.add(b.tri(tuple(c), tuple(c + e[0]), tuple(c + e[1]), red if rng.uniform() < 0.5 else white))
+    w.add(b.bvh(mesh, 0.0, 1.0, axis_seed=9))
+    w.add(b.xz_rect(0, 555, 0, 555, 0, white))
+    if not suspend:
+        for i in range(10):
+            w.add(b.sphere((1000.0 + 10 * i, 2000.0, 3000.0), 1.0, white))
+    scene = b.finish(w)
+    basis = rt.CameraBasis(origin=(278.0, 278.0, 200.0), horizontal=(556.0, 0.0, 0.0), vertical=(0.0, 556.0, 0.0),
+                           lower_left_corner=(0.0, 0.0, 200.0), u=(1.0, 0.0, 0.0), v=(0.0, 1.0, 0.0),
+                           lens_radius=0.0, time_start=0.0, time_end=0.0)
+    params = rt.render_params(40, 30, 3, 8, background=(0.05, 0.05, 0.08), seed=13)
+    want, cnt = orc.render(scene, basis, params)
+    assert np.isfinite(want).all() and (want > 0).any()
+    capfd.readouterr()
+    with rt.options(launch_log=1):
+        got, st = gpu_render(rt, scene, basis, params)
+    err = capfd.readouterr().err
+    np.testing.assert_array_equal(got, want)
+    assert st["segments"] == cnt["segments"]
+    replayed = sum(int(x.split("chunk")[1].split(":")[1].split()[0]) for x in err.splitlines()
+                   if "samples replayed" in x)
+    assert replayed == 40 * 30 * 3, (replayed, err[-2000:])
+
+
 def _c4_with_spheres(rt):
     """cornell_boundaries + a triangle mesh BVH (a tetrahedral fan around (325, 100, 200)) + a
     top-level sphere run, built through SceneBuilder so that the scene has spheres and
