@@ -1440,6 +1440,11 @@ RT_DEV bool bvh_hit(const DevScene& S, float delta, uint32_t root, const Ray& r,
 // false; the walk resumes it on a later trip of the sample loop, together with the lanes
 // that reach the same BVH then. The visit order and every value are unchanged, only when a
 // visit runs differs, so the result is the same bits.
+#ifndef RT_POP_PREFETCH
+#define RT_POP_PREFETCH 0
+#endif
+template <uint32_t kF>
+constexpr bool kPopPrefetch = RT_POP_PREFETCH && (kF & (kFTri | kFDeep)) == 0u;
 template <int kKind, uint32_t kF, bool kSusp>
 RT_DEV bool bvh_run(const DevScene& S, float delta, const f4* wrapper, const Ray& r, V inv, float tmin, float& closest,
                     uint32_t& hit_code, uint32_t* stk, uint32_t mode, Trav& tv, uint32_t susp) {
@@ -1543,6 +1548,15 @@ RT_DEV bool bvh_run(const DevScene& S, float delta, const f4* wrapper, const Ray
 #ifdef RT_PROFILE_REGIONS
         ++visits;
 #endif
+        // RT_POP_PREFETCH (A/B): the stack top read at the start of the trip, beside the node loads. A trip
+        // that pops has pushed nothing, so the first entry its pop loop takes is this one.
+        [[maybe_unused]] uint32_t pf_node = 0u;
+        [[maybe_unused]] float pf_t = 0.0f;
+        if constexpr (kPopPrefetch<kF>) {
+            const uint32_t top = (sp > 0u ? sp - 1u : 0u) * 128u;
+            pf_node = stk[top];
+            pf_t = __uint_as_float(stk[top + 64u]);
+        }
         PROF_T0(pt);
         if (lnode != kNoNode) {
             // The 1-2 leaf children of ONE reference BVH2 node, left then right,
@@ -1708,11 +1722,16 @@ RT_DEV bool bvh_run(const DevScene& S, float delta, const f4* wrapper, const Ray
         PROF_T0(ppop);
         if (popnext) {
             bool found = false;
+            [[maybe_unused]] bool first = true;
             while (sp > 0u) {
                 sp -= 1u;
                 uint32_t cand;
                 float tenter;
-                if (!(kF & kFDeep) || sp < S.stack_depth) {
+                if (kPopPrefetch<kF> && first) {
+                    cand = pf_node;
+                    tenter = pf_t;
+                    first = false;
+                } else if (!(kF & kFDeep) || sp < S.stack_depth) {
                     cand = stk[sp * 128u];
                     tenter = __uint_as_float(stk[sp * 128u + 64u]);
                 } else {
